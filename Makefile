@@ -1,0 +1,38 @@
+# Builds the gfx950 HIP library of the YOLOv11 inference path in-tree.
+#   make            -> yolo-infer-pt_amd/yolo_hip/libyolo_hip.so
+#   make oracle     -> oracle/_c/liboracle_nms.so (CPU checker, tests only)
+ROCM ?= /opt/rocm
+HIPCC ?= $(ROCM)/bin/hipcc
+ARCH ?= gfx950
+PKG := yolo-infer-pt_amd
+SRC := $(PKG)/csrc
+OUT := $(PKG)/yolo_hip/libyolo_hip.so
+OBJDIR := build/obj
+HIPFLAGS := --offload-arch=$(ARCH) -O3 -fPIC -std=c++17 -Iinclude -I$(SRC) \
+            -fhip-fp32-correctly-rounded-divide-sqrt -Wno-unused-result
+OBJS := $(OBJDIR)/engine.o $(OBJDIR)/conv.o $(OBJDIR)/misc.o $(OBJDIR)/nms.o
+
+all: $(OUT)
+
+$(OBJDIR):
+	mkdir -p $(OBJDIR)
+
+$(OBJDIR)/engine.o: $(SRC)/engine.cpp $(SRC)/common.h include/yolo_hip.h | $(OBJDIR)
+	$(HIPCC) $(HIPFLAGS) -x hip -c $< -o $@
+
+$(OBJDIR)/conv.o: $(SRC)/conv.hip $(SRC)/common.h $(SRC)/dtypes.h | $(OBJDIR)
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+$(OBJDIR)/misc.o: $(SRC)/misc.hip $(SRC)/common.h $(SRC)/dtypes.h | $(OBJDIR)
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+$(OBJDIR)/nms.o: $(SRC)/nms.hip $(SRC)/common.h $(SRC)/dtypes.h | $(OBJDIR)
+	$(HIPCC) $(HIPFLAGS) -ffp-contract=off -c $< -o $@
+
+$(OUT): $(OBJS)
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $(OBJS)
+
+clean:
+	rm -rf build $(OUT)
+
+.PHONY: all clean

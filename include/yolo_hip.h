@@ -1,0 +1,163 @@
+/*
+ * yolo_hip.h — C ABI of the MI355X (gfx950) YOLOv11 inference path.
+ *
+ * This is the drop-in boundary between the Python mirror of the reference's
+ * module API (yolo-infer-pt_amd/nets/nn.py, yolo-infer-pt_amd/utils/util.py)
+ * and the hand-written HIP kernels in yolo-infer-pt_amd/csrc/.  Signatures use
+ * plain pointers and sizes only; no torch types cross this line.
+ *
+ * Reference interfaces replaced (file:line into t0saki/YOLO-Infer-pt):
+ *   yh_create           nets/nn.py:308-347  yolo_v11_{n,t,s,m,l,x}() -> YOLO(width, depth, csp, nc)
+ *                       nets/nn.py:282-292  YOLO.__init__ (DarkNet + DarkFPN + Head graph)
+ *   yh_conv_count,
+ *   yh_conv_info        the reference's state_dict naming (nets/nn.py module tree), one entry per conv
+ *   yh_load_conv        nets/nn.py:8-25     fuse_conv (BN folded into conv in fp32), nets/nn.py:299-305 YOLO.fuse
+ *   yh_forward          nets/nn.py:294-297  YOLO.forward in eval mode, incl. Head.forward decode
+ *                       (nets/nn.py:255-270), DFL (nets/nn.py:222-225) and make_anchors (utils/util.py:85-96)
+ *   yh_nms              utils/util.py:123-169 non_max_suppression (+ torchvision.ops.nms, util.py:162)
+ *
+ * Conventions
+ *   - Every function returns 0 on success and a negative YH_E* code on failure;
+ *     yh_last_error() returns a thread-local message describing the last failure.
+ *   - Device pointers are HIP device memory owned by the caller (PyTorch tensors).
+ *     The library owns its packed weights and its activation workspace.
+ *   - `stream` is a hipStream_t passed as void* (0 = legacy default stream).
+ *     yh_forward and yh_nms are asynchronous on that stream: they never
+ *     synchronise the host and allocate nothing once the workspace for a
+ *     given (batch, height, width) exists.
+ *   - One handle is bound to one device and one compute dtype.  Calls on one
+ *     handle must be serialised by the caller; distinct handles are independent
+ *     (data-parallel serving = one handle per GPU).
+ */
+#ifndef YOLO_HIP_H
+#define YOLO_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define YH_ABI_VERSION 1
+
+/* status codes */
+#define YH_OK 0
+#define YH_EINVAL -1     /* bad argument / shape */
+#define YH_ESTATE -2     /* call out of order (e.g. forward before all weights loaded) */
+#define YH_EHIP -3       /* HIP runtime error */
+#define YH_ENOMEM -4     /* device allocation failed */
+
+/* compute / storage dtypes of a handle (activations and outputs) */
+#define YH_F32 0
+#define YH_F16 1
+#define YH_BF16 2
+
+typedef struct yh_handle yh_handle;
+
+/* Network description: the (width, depth, csp) triple of nets/nn.py:308-347 plus
+ * the class count (Head nc, nets/nn.py:232-238). */
+typedef struct {
+    int width[6];     /* e.g. {3,16,32,64,128,256} for v11_n */
+    int depth[6];     /* repeat counts; only depth[0..5] as used by DarkNet/DarkFPN */
+    int csp[2];       /* 0/1: C3k nesting for shallow / deep C3k2 blocks */
+    int num_classes;  /* nc */
+} yh_variant;
+
+/* ABI version of the loaded library (YH_ABI_VERSION). */
+int yh_abi_version(void);
+
+/* Thread-local message of the last failing call ("" if none). */
+const char* yh_last_error(void);
+
+/* Build the layer graph of a variant for `device` in `dtype` (YH_F32/F16/BF16). */
+int yh_create(const yh_variant* variant, int device, int dtype, yh_handle** out);
+
+/* Release all device memory owned by the handle. NULL is accepted. */
+void yh_destroy(yh_handle* h);
+
+/* Number of convolutions whose weights the handle expects. */
+int yh_conv_count(const yh_handle* h);
+
+/* Describe conv `index`: `name` = state_dict prefix of the owning module
+ * (e.g. "net.p2.1.res_m.0.conv1" for a Conv block, "head.box.0.2" for a plain
+ * nn.Conv2d); shape of the expected fp32 weight (cout, cin_per_group, k, k);
+ * `has_bias` = 1 if the reference module carries a conv bias (head output
+ * convs). The pointer in *name stays valid for the handle's lifetime. */
+int yh_conv_info(const yh_handle* h, int index, const char** name, int* cout,
+                 int* cin_per_group, int* ksize, int* groups, int* has_bias);
+
+/* Load one conv from host fp32 arrays. `weight` is (cout, cin/groups, k, k)
+ * contiguous. `bias` may be NULL (treated as zeros). If `bn_gamma` is non-NULL
+ * the BatchNorm (gamma, beta, running mean, running var, eps) is folded in
+ * exactly as fuse_conv (nets/nn.py:8-25) does it, in fp32. Packed, dtype-cast
+ * copies are uploaded to the handle's device; host arrays may be freed after. */
+int yh_load_conv(yh_handle* h, int index, const float* weight, const float* bias,
+                 const float* bn_gamma, const float* bn_beta, const float* bn_mean,
+                 const float* bn_var, double bn_eps);
+
+/* Anchors produced for an input of height x width (sum over strides 8/16/32). */
+int yh_num_anchors(const yh_handle* h, int height, int width, int* anchors);
+
+/* Bytes of device workspace the handle holds for (batch, height, width)
+ * after yh_reserve (activations, excluding weights). */
+int yh_workspace_bytes(const yh_handle* h, int batch, int height, int width, size_t* bytes);
+
+/* Optional: allocate the workspace for (batch, height, width) up front. */
+int yh_reserve(yh_handle* h, int batch, int height, int width);
+
+/* Eval-mode forward.
+ *   x: device (batch, 3, height, width) NCHW contiguous, handle dtype
+ *   y: device (batch, 4 + nc, anchors) contiguous, handle dtype:
+ *      rows 0..3 = (cx, cy, w, h) in pixels, rows 4.. = sigmoid class scores
+ * height, width: multiples of 32. */
+int yh_forward(yh_handle* h, const void* x, int batch, int height, int width,
+               void* y, void* stream);
+
+/* Bytes of device workspace yh_nms needs for a (batch, 4 + num_classes, anchors) input. */
+size_t yh_nms_workspace_bytes(int batch, int num_classes, int anchors);
+
+/* Batched NMS over a head output y (batch, 4 + num_classes, anchors) of dtype
+ * YH_F32/F16/BF16, on the current HIP device. Stateless: the caller supplies the
+ * workspace (yh_nms_workspace_bytes). Semantics of non_max_suppression
+ * (utils/util.py:123-169): candidate (anchor, class) pairs with score >
+ * conf_threshold (threshold rounded to the input dtype, as torch compares),
+ * sorted by score descending (ties: lower anchor*nc + class first), truncated to
+ * max_nms, class-offset boxes (class * max_wh), greedy IoU > iou_threshold
+ * suppression (torchvision.ops.nms contract), at most max_det kept per image.
+ *   dets:   device float (batch, max_det, 6) = x1, y1, x2, y2, score, class
+ *   counts: device int32 (batch) kept detections per image
+ * Box geometry is evaluated in fp32 for every dtype; class scores must lie in
+ * [0, 2) (sigmoid outputs). Asynchronous on `stream`. */
+int yh_nms(int dtype, const void* y, int batch, int num_classes, int anchors,
+           float conf_threshold, double iou_threshold, int max_det, int max_nms,
+           float max_wh, void* workspace, size_t workspace_bytes,
+           float* dets, int* counts, void* stream);
+
+/* Per-op instrumentation (bench / roofline). With profiling enabled,
+ * yh_forward launches the ops eagerly with a HIP event pair around each op on
+ * the caller's stream, synchronises at the end and accumulates per-op elapsed
+ * milliseconds. Disabled by default (forward then runs as a HIP graph). */
+int yh_profile_enable(yh_handle* h, int enable);
+int yh_profile_reset(yh_handle* h);
+
+/* Number of ops (kernel launch groups) in the forward. */
+int yh_op_count(const yh_handle* h);
+
+/* Describe op `index` for an input of (batch, height, width): label (module
+ * path), class (0 dense 3x3 conv, 1 dense 1x1 conv, 2 stem conv, 3 depthwise,
+ * 4 SPPF pools, 5 PSA attention, 6 head decode), algorithmic bytes (each
+ * operand read once, each output written once, handle dtype) and FLOPs per
+ * call, accumulated profiled milliseconds and call count. */
+int yh_op_info(const yh_handle* h, int index, int batch, int height, int width,
+               const char** label, int* op_class, double* bytes, double* flops,
+               double* ms_total, int* calls);
+
+/* Use a captured HIP graph for yh_forward (default on). */
+int yh_set_graph(yh_handle* h, int enable);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* YOLO_HIP_H */

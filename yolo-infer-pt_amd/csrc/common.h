@@ -1,0 +1,102 @@
+// Shared device-side types and launcher declarations for the gfx950 YOLOv11 path.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace yh {
+
+enum DType { F32 = 0, F16 = 1, BF16 = 2 };
+inline int dtype_size(int dt) { return dt == F32 ? 4 : 2; }
+
+enum Act { ACT_ID = 0, ACT_SILU = 1 };
+
+// Dense conv as an implicit GEMM over NHWC activations.
+//   GEMM rows M  = batch * Ho * Wo (output pixels)
+//   GEMM cols N  = Cout (physical, multiple of 8)
+//   reduction K  = KH * KW * Cin (Cin physical, multiple of 8), packed weights
+//                  are [Coutp][Kp] with k = (kh*KW + kw)*Cin + ci, zero padded.
+// The input may be the channel-concatenation of two NHWC views ("segments");
+// a segment may be read through a nearest x2 upsample (up = 1), which is how
+// DarkFPN's up+cat (nets/nn.py:203-209) is fused into the consumer's loader.
+struct ConvArgs {
+    const void* in0; int ldc0, c0, up0, h0, w0;   // segment 0: channels [0, c0)
+    const void* in1; int ldc1, c1, up1, h1, w1;   // segment 1: channels [c0, c0+c1)
+    int Hi, Wi, Ho, Wo, stride, pad, KH, KW, Cin, K, Kp, M;
+    const void* w;       // packed weights, handle dtype
+    const float* bias;   // [Coutp] fp32
+    const int* ktab;     // [Kp/8]: (kh<<24)|(kw<<16)|ci, ci=0xffff for padding
+    void* out; int ldo;  // output view base (channel offset applied), pixel stride
+    const void* res; int ldr;  // optional residual view added after the activation
+    int Cout;            // physical output channels written (multiple of 8)
+    int act;
+    int gm, gn;          // tile grid
+};
+
+// First layer: 3-channel NCHW input (the caller's tensor), 3x3 stride-2 conv.
+struct FirstConvArgs {
+    const void* const* io;  // io[0] = x (NCHW), read at kernel start (graph-replay friendly)
+    int H, W, Ho, Wo, Cout, ldo, M;
+    const float* w;      // [Cout][27] fp32 (ci, kh, kw)
+    const float* bias;   // [Cout]
+    void* out;
+    int act;
+};
+
+// Depthwise 3x3 stride-1 conv on an NHWC view.
+struct DwArgs {
+    const void* in; int ldi;
+    int H, W, C, M;
+    const float* w;      // [9][C] fp32
+    const float* bias;   // [C]
+    void* out; int ldo;
+    int act;
+};
+
+// SPPF: y1 = mp5(x), y2 = mp5(y1), y3 = mp5(y2) (nets/nn.py:90-94) from slice 0
+// of a 4-slice concat buffer into slices 1..3.
+struct PoolArgs {
+    void* buf; int ldc, C, H, W, B;
+};
+
+// C2PSA attention (nets/nn.py:111-123) with the positional depthwise conv fused:
+// out[:, h*dh + d] = softmax(q^T k * scale) v  +  pe(v)
+struct AttnArgs {
+    const void* qkv; int ldq;   // per head: [q(dk) | k(dk) | v(dh)]
+    int T, Hs, Ws, heads, dk, dh;
+    float scale;
+    const float* pe_w;   // [9][heads*dh]
+    const float* pe_b;   // [heads*dh]
+    void* out; int ldo;
+};
+
+// Detect-head decode (nets/nn.py:255-270, DFL 222-225, make_anchors util.py:85-96).
+struct DecodeArgs {
+    const void* lvl[3]; int ldc; int H[3], W[3]; float stride[3];
+    int nc, A, B;
+    const void* const* io;  // io[1] = y (B, 4+nc, A)
+};
+
+// NMS (utils/util.py:123-169)
+struct NmsArgs {
+    const void* y; int B, A, nc;
+    float conf;          // threshold, already rounded to the input dtype
+    float iou;           // largest float <= iou threshold (so ovr > iou  <=>  ovr > thr)
+    float max_wh;
+    int max_det, max_nms;
+    unsigned long long* keys;  // [B][A*nc] candidate keys
+    int* counts;               // [B] candidate counts (zeroed by the launcher)
+    float* dets; int* ndet;
+};
+
+// launchers (return hipError_t as int)
+int launch_conv(int dtype, int BM, int BN, const ConvArgs& a, hipStream_t s);
+int conv_lds_bytes(int dtype, int BM, int BN, int Kp);
+int launch_first_conv(int dtype, const FirstConvArgs& a, int B, hipStream_t s);
+int launch_dwconv(int dtype, const DwArgs& a, hipStream_t s);
+int launch_sppf(int dtype, const PoolArgs& a, hipStream_t s);
+int launch_attention(int dtype, const AttnArgs& a, int B, hipStream_t s);
+int launch_decode(int dtype, const DecodeArgs& a, hipStream_t s);
+int launch_set_io(void** io, const void* x, void* y, hipStream_t s);
+int launch_nms(int dtype, const NmsArgs& a, hipStream_t s);
+
+}  // namespace yh

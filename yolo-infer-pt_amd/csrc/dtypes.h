@@ -1,0 +1,97 @@
+// Device-side dtype traits: storage types, 8-element chunk moves, MFMA step.
+#pragma once
+#include <hip/hip_runtime.h>
+
+namespace yh {
+
+typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
+typedef __attribute__((ext_vector_type(8))) _Float16 f16x8;
+typedef __attribute__((ext_vector_type(4))) float f32x4;
+
+// A "chunk" = 8 consecutive channels of one pixel = 16 B for 2-byte types, 32 B for f32.
+template <typename T> struct Chunk { uint4 v[sizeof(T) / 2]; };
+
+template <typename T>
+__device__ __forceinline__ Chunk<T> ld_chunk(const T* p) {
+    Chunk<T> c;
+    const uint4* q = reinterpret_cast<const uint4*>(p);
+#pragma unroll
+    for (int i = 0; i < (int)(sizeof(T) / 2); ++i) c.v[i] = q[i];
+    return c;
+}
+template <typename T>
+__device__ __forceinline__ void st_chunk(T* p, const Chunk<T>& c) {
+    uint4* q = reinterpret_cast<uint4*>(p);
+#pragma unroll
+    for (int i = 0; i < (int)(sizeof(T) / 2); ++i) q[i] = c.v[i];
+}
+template <typename T>
+__device__ __forceinline__ Chunk<T> zero_chunk() {
+    Chunk<T> c;
+#pragma unroll
+    for (int i = 0; i < (int)(sizeof(T) / 2); ++i) c.v[i] = make_uint4(0, 0, 0, 0);
+    return c;
+}
+
+template <typename T> __device__ __forceinline__ float tof(T v) { return (float)v; }
+template <typename T> __device__ __forceinline__ T fromf(float v) { return (T)v; }
+
+template <typename T>
+__device__ __forceinline__ void chunk_to_f(const Chunk<T>& c, float (&f)[8]) {
+    const T* e = reinterpret_cast<const T*>(&c);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) f[i] = tof(e[i]);
+}
+template <typename T>
+__device__ __forceinline__ Chunk<T> f_to_chunk(const float (&f)[8]) {
+    Chunk<T> c;
+    T* e = reinterpret_cast<T*>(&c);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) e[i] = fromf<T>(f[i]);
+    return c;
+}
+
+// SiLU: exact-rounded exp/div on the f32 (parity) path, hardware exp/rcp on 16-bit paths.
+template <typename T> __device__ __forceinline__ float silu(float x) {
+    return x * __builtin_amdgcn_rcpf(1.0f + __expf(-x));
+}
+template <> __device__ __forceinline__ float silu<float>(float x) { return x / (1.0f + expf(-x)); }
+
+// One 16(rows) x 16(cols) x 32(k) MFMA step. a/b point at a lane's 8 consecutive
+// k values of its row (A) / column (B). For f32 the 32-deep step is eight exact
+// f32 MFMAs (16x16x4); the k permutation is the same for A and B, so the sum is
+// over the same 32 products.
+template <typename T> struct Mma;
+template <> struct Mma<__bf16> {
+    static __device__ __forceinline__ void step(f32x4& acc, const uint4* a, const uint4* b) {
+        bf16x8 av = __builtin_bit_cast(bf16x8, a[0]);
+        bf16x8 bv = __builtin_bit_cast(bf16x8, b[0]);
+        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av, bv, acc, 0, 0, 0);
+    }
+};
+template <> struct Mma<_Float16> {
+    static __device__ __forceinline__ void step(f32x4& acc, const uint4* a, const uint4* b) {
+        f16x8 av = __builtin_bit_cast(f16x8, a[0]);
+        f16x8 bv = __builtin_bit_cast(f16x8, b[0]);
+        acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(av, bv, acc, 0, 0, 0);
+    }
+};
+template <> struct Mma<float> {
+    static __device__ __forceinline__ void step(f32x4& acc, const uint4* a, const uint4* b) {
+        const float* af = reinterpret_cast<const float*>(a);
+        const float* bf = reinterpret_cast<const float*>(b);
+#pragma unroll
+        for (int kk = 0; kk < 8; ++kk)
+            acc = __builtin_amdgcn_mfma_f32_16x16x4f32(af[kk], bf[kk], acc, 0, 0, 0);
+    }
+};
+
+// XCD-aware bijective remap of a 1-D block id: blocks b and b+8 share an XCD
+// (round-robin dispatch), so give each XCD a contiguous range of logical ids.
+__device__ __forceinline__ int xcd_remap(int bid, int nwg) {
+    const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
+    const int base = xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q;
+    return base + (bid >> 3);
+}
+
+}  // namespace yh

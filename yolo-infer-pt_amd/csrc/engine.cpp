@@ -1,0 +1,989 @@
+// Host runtime of the gfx950 YOLOv11 path: builds the layer graph of a variant
+// (mirroring the reference module tree, nets/nn.py:28-305), folds BatchNorm into
+// the convs exactly like fuse_conv (nets/nn.py:8-25), packs weights for the
+// implicit-GEMM kernels, owns the NHWC activation workspace, launches the
+// kernels (optionally as one captured HIP graph) and exports the C ABI
+// declared in include/yolo_hip.h.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <memory>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "common.h"
+#include "yolo_hip.h"
+
+namespace yh {
+
+static thread_local std::string g_err;
+
+struct Fail : std::runtime_error {
+    int code;
+    Fail(int c, const std::string& m) : std::runtime_error(m), code(c) {}
+};
+
+#define HIPCHECK(expr)                                                                 \
+    do {                                                                               \
+        hipError_t e__ = (expr);                                                       \
+        if (e__ != hipSuccess)                                                         \
+            throw Fail(YH_EHIP, std::string(#expr) + ": " + hipGetErrorString(e__));   \
+    } while (0)
+
+static void require(bool ok, const std::string& msg, int code = YH_EINVAL) {
+    if (!ok) throw Fail(code, msg);
+}
+
+static int round_up(int v, int m) { return (v + m - 1) / m * m; }
+
+// ---------------------------------------------------------------- dtype casts
+static uint16_t f2bf(float f) {
+    uint32_t u;
+    std::memcpy(&u, &f, 4);
+    if ((u & 0x7fffffffu) > 0x7f800000u) return (uint16_t)((u >> 16) | 0x40);  // NaN
+    u += 0x7fffu + ((u >> 16) & 1u);
+    return (uint16_t)(u >> 16);
+}
+static uint16_t f2h(float f) {
+    uint32_t x;
+    std::memcpy(&x, &f, 4);
+    const uint32_t sign = (x >> 16) & 0x8000u;
+    const uint32_t ax = x & 0x7fffffffu;
+    if (ax >= 0x7f800000u) return (uint16_t)(sign | 0x7c00u | (ax > 0x7f800000u ? 0x200u : 0u));
+    if (ax >= 0x477ff000u) return (uint16_t)(sign | 0x7c00u);  // rounds to inf
+    if (ax < 0x38800000u) {  // subnormal / zero in half
+        float af;
+        std::memcpy(&af, &ax, 4);
+        const float scaled = af * 16777216.0f;  // 2^24: half subnormal unit = 2^-24
+        const uint32_t m = (uint32_t)std::nearbyint(scaled);
+        return (uint16_t)(sign | m);
+    }
+    uint32_t e = ((ax >> 23) - 112u) << 10;
+    uint32_t m = (ax >> 13) & 0x3ffu;
+    uint32_t h = e | m;
+    const uint32_t rem = ax & 0x1fffu;
+    if (rem > 0x1000u || (rem == 0x1000u && (h & 1u))) ++h;
+    return (uint16_t)(sign | h);
+}
+
+// ---------------------------------------------------------------- graph model
+enum ConvKind { CK_DENSE = 0, CK_FIRST = 1, CK_DW = 2, CK_PE = 3 };
+enum OpKind { OP_FIRST, OP_CONV, OP_DW, OP_SPPF, OP_ATTN, OP_DECODE };
+enum OpClass { CL_CONV3 = 0, CL_CONV1 = 1, CL_FIRST = 2, CL_DW = 3, CL_SPPF = 4, CL_ATTN = 5, CL_DECODE = 6, CL_N = 7 };
+
+struct Tensor { int level; int C; };        // physical channels = pixel stride
+struct View { int t = -1; int coff = 0; int C = 0; };
+
+struct Seg { View v; int up = 0; };
+
+struct ConvDesc {
+    std::string name;
+    ConvKind kind;
+    int cout, cin, k, stride, groups, has_bias, act;
+    std::vector<std::pair<int, int>> segs;   // (logical, physical) channel counts of the input
+    int cin_p = 0, cout_p = 0, K = 0, Kp = 0, coutp_pad = 0;
+    bool loaded = false;
+    std::vector<float> wf, bf;  // folded fp32 weights (cout, cin/g, k, k) and bias (cout)
+    void* w_dev = nullptr;
+    float* b_dev = nullptr;
+    int* ktab_dev = nullptr;
+};
+
+struct Op {
+    OpKind kind;
+    int conv = -1;
+    std::vector<Seg> in;
+    View out, res;
+    bool has_res = false;
+    int heads = 0;
+    View lvl[3];
+    std::string label;
+};
+
+struct Workspace {
+    int B = 0, H = 0, W = 0;
+    void* base = nullptr;
+    size_t bytes = 0;
+    std::vector<size_t> off;  // per tensor
+};
+
+struct GraphKey {
+    int B, H, W;
+    bool operator<(const GraphKey& o) const {
+        return B != o.B ? B < o.B : (H != o.H ? H < o.H : W < o.W);
+    }
+};
+
+struct Net {
+    yh_variant var;
+    int device, dtype, es;
+    std::vector<Tensor> tensors;
+    std::vector<ConvDesc> convs;
+    std::vector<Op> ops;
+    Workspace ws;
+    void** io_dev = nullptr;      // {x, y}
+    bool use_graph = true;
+    std::map<GraphKey, hipGraphExec_t> graphs;
+    hipStream_t cap_stream = nullptr;
+    bool profile = false;
+    std::vector<double> prof_ms;
+    std::vector<int> prof_calls;
+    std::vector<hipEvent_t> ev;
+    int lastB = 0, lastH = 0, lastW = 0;
+
+    // ---------------------------------------------------------- builder
+    int tensor(int level, int C) {
+        tensors.push_back({level, round_up(C, 8)});
+        return (int)tensors.size() - 1;
+    }
+    View full(int t, int C = -1) {
+        View v;
+        v.t = t;
+        v.coff = 0;
+        v.C = C < 0 ? tensors[t].C : C;
+        return v;
+    }
+    View slice(int t, int coff, int C) {
+        require(coff % 8 == 0 && C % 8 == 0, "concat slice not a multiple of 8 channels");
+        View v;
+        v.t = t;
+        v.coff = coff;
+        v.C = C;
+        return v;
+    }
+    int new_conv(const std::string& name, ConvKind kind, int cin, int cout, int k, int s, int g, int has_bias, int act) {
+        ConvDesc d;
+        d.name = name;
+        d.kind = kind;
+        d.cin = cin; d.cout = cout; d.k = k; d.stride = s; d.groups = g;
+        d.has_bias = has_bias; d.act = act;
+        convs.push_back(std::move(d));
+        return (int)convs.size() - 1;
+    }
+    // dense conv op (k in {1,3}), input segments given as (view, logical channels, upsample)
+    void dense(const std::string& name, const std::vector<Seg>& in, const std::vector<int>& logical, int cout, int k,
+               int s, int act, View out, const View* res = nullptr, int has_bias = 0) {
+        int cin = 0;
+        for (int c : logical) cin += c;
+        const int ci = new_conv(name, CK_DENSE, cin, cout, k, s, 1, has_bias, act);
+        ConvDesc& d = convs[ci];
+        for (size_t i = 0; i < in.size(); ++i) d.segs.push_back({logical[i], in[i].v.C});
+        require(in.size() <= 2, "at most two concat segments");
+        if (in.size() == 2) require(logical[0] == in[0].v.C && logical[0] % 8 == 0, "segment 0 must be 8-aligned");
+        Op op;
+        op.kind = OP_CONV;
+        op.conv = ci;
+        op.in = in;
+        op.out = out;
+        if (res) { op.res = *res; op.has_res = true; }
+        op.label = name;
+        ops.push_back(op);
+    }
+    View conv1(const std::string& name, View x, int xc, int cout, int act, View out, const View* res = nullptr) {
+        dense(name, {Seg{x, 0}}, {xc}, cout, 1, 1, act, out, res);
+        return out;
+    }
+    View conv3(const std::string& name, View x, int xc, int cout, int s, int act, View out, const View* res = nullptr) {
+        dense(name, {Seg{x, 0}}, {xc}, cout, 3, s, act, out, res);
+        return out;
+    }
+
+    // Residual (nn.py:42-49): out = x + conv2(conv1(x)), both 3x3 SiLU
+    void residual(const std::string& p, View x, int ch, double e, View out, int level) {
+        const int hid = (int)(ch * e);
+        const int t = tensor(level, hid);
+        conv3(p + ".conv1", x, ch, hid, 1, ACT_SILU, full(t));
+        conv3(p + ".conv2", full(t), hid, ch, 1, ACT_SILU, out, &x);
+    }
+    // CSPModule / C3k (nn.py:52-63)
+    void cspmodule(const std::string& p, View x, int in_ch, int out_ch, View out, int level) {
+        const int h = out_ch / 2;
+        const int t = tensor(level, 2 * h);
+        View a = slice(t, 0, h), b = slice(t, h, h);
+        conv1(p + ".conv1", x, in_ch, h, ACT_SILU, a);
+        conv1(p + ".conv2", x, in_ch, h, ACT_SILU, b);
+        residual(p + ".res_m.0", a, h, 1.0, a, level);
+        residual(p + ".res_m.1", a, h, 1.0, a, level);
+        conv1(p + ".conv3", full(t), 2 * h, out_ch, ACT_SILU, out);
+    }
+    // CSP / C3k2 (nn.py:66-80); input may be a 2-segment (optionally upsampled) concat
+    void csp(const std::string& p, const std::vector<Seg>& in, const std::vector<int>& logical, int out_ch, int n,
+             bool use_c3k, int r, View out, int level) {
+        const int c = out_ch / r;
+        const int t = tensor(level, (2 + n) * c);
+        dense(p + ".conv1", in, logical, 2 * c, 1, 1, ACT_SILU, slice(t, 0, 2 * c));
+        for (int i = 0; i < n; ++i) {
+            View src = slice(t, (1 + i) * c, c), dst = slice(t, (2 + i) * c, c);
+            const std::string q = p + ".res_m." + std::to_string(i);
+            if (!use_c3k) residual(q, src, c, 0.5, dst, level);
+            else cspmodule(q, src, c, c, dst, level);
+        }
+        conv1(p + ".conv2", full(t), (2 + n) * c, out_ch, ACT_SILU, out);
+    }
+    // SPP / SPPF (nn.py:83-94)
+    void sppf(const std::string& p, View x, int in_ch, int out_ch, View out, int level) {
+        const int h = in_ch / 2;
+        const int t = tensor(level, 4 * h);
+        conv1(p + ".conv1", x, in_ch, h, ACT_SILU, slice(t, 0, h));
+        Op op;
+        op.kind = OP_SPPF;
+        op.out = slice(t, 0, h);
+        op.label = p + ".res_m";
+        ops.push_back(op);
+        conv1(p + ".conv2", full(t), 4 * h, out_ch, ACT_SILU, out);
+    }
+    // PSABlock (nn.py:126-136), in place on view x
+    void psablock(const std::string& p, View x, int ch, int heads, int level) {
+        const int dh = ch / heads, dk = dh / 2;
+        require(dh == 64 && dk == 32, "PSA head dims must be dh=64, dk=32");
+        const int qc = ch + 2 * dk * heads;
+        const int tq = tensor(level, qc);
+        conv1(p + ".conv1.qkv", x, ch, qc, ACT_ID, full(tq));
+        const int ta = tensor(level, ch);
+        const int pe = new_conv(p + ".conv1.conv1", CK_PE, ch, ch, 3, 1, ch, 0, ACT_ID);
+        Op op;
+        op.kind = OP_ATTN;
+        op.conv = pe;
+        op.in = {Seg{full(tq), 0}};
+        op.out = full(ta);
+        op.heads = heads;
+        op.label = p + ".conv1";
+        ops.push_back(op);
+        conv1(p + ".conv1.conv2", full(ta), ch, ch, ACT_ID, x, &x);
+        const int tf = tensor(level, 2 * ch);
+        conv1(p + ".conv2.0", x, ch, 2 * ch, ACT_SILU, full(tf));
+        conv1(p + ".conv2.1", full(tf), 2 * ch, ch, ACT_ID, x, &x);
+    }
+    // PSA / C2PSA (nn.py:139-148)
+    void psa(const std::string& p, View x, int ch, int n, View out, int level) {
+        const int half = ch / 2;
+        const int t = tensor(level, 2 * half);
+        conv1(p + ".conv1", x, ch, 2 * half, ACT_SILU, full(t));
+        for (int i = 0; i < n; ++i) psablock(p + ".res_m." + std::to_string(i), slice(t, half, half), half, ch / 128, level);
+        conv1(p + ".conv2", full(t), 2 * half, ch, ACT_SILU, out);
+    }
+
+    void build() {
+        const int* w = var.width;
+        const int* d = var.depth;
+        const bool c0 = var.csp[0] != 0, c1 = var.csp[1] != 0;
+        const int nc = var.num_classes;
+        // ---- DarkNet (nn.py:151-189)
+        const int t1 = tensor(1, w[1]);
+        {
+            const int ci = new_conv("net.p1.0", CK_FIRST, w[0], w[1], 3, 2, 1, 0, ACT_SILU);
+            Op op;
+            op.kind = OP_FIRST;
+            op.conv = ci;
+            op.out = full(t1, w[1]);
+            op.label = "net.p1.0";
+            ops.push_back(op);
+        }
+        const int t2 = tensor(2, w[2]);
+        conv3("net.p2.0", full(t1, w[1]), w[1], w[2], 2, ACT_SILU, full(t2, w[2]));
+        const int t2b = tensor(2, w[3]);
+        csp("net.p2.1", {Seg{full(t2, w[2]), 0}}, {w[2]}, w[3], d[0], c0, 4, full(t2b, w[3]), 2);
+        const int t3 = tensor(3, w[3]);
+        conv3("net.p3.0", full(t2b, w[3]), w[3], w[3], 2, ACT_SILU, full(t3, w[3]));
+        const int b3 = tensor(3, w[4]);
+        csp("net.p3.1", {Seg{full(t3, w[3]), 0}}, {w[3]}, w[4], d[1], c0, 4, full(b3, w[4]), 3);
+        const int t4 = tensor(4, w[4]);
+        conv3("net.p4.0", full(b3, w[4]), w[4], w[4], 2, ACT_SILU, full(t4, w[4]));
+        const int b4 = tensor(4, w[4]);
+        csp("net.p4.1", {Seg{full(t4, w[4]), 0}}, {w[4]}, w[4], d[2], c1, 2, full(b4, w[4]), 4);
+        const int t5 = tensor(5, w[5]);
+        conv3("net.p5.0", full(b4, w[4]), w[4], w[5], 2, ACT_SILU, full(t5, w[5]));
+        const int t5b = tensor(5, w[5]);
+        csp("net.p5.1", {Seg{full(t5, w[5]), 0}}, {w[5]}, w[5], d[3], c1, 2, full(t5b, w[5]), 5);
+        const int t5c = tensor(5, w[5]);
+        sppf("net.p5.2", full(t5b, w[5]), w[5], w[5], full(t5c, w[5]), 5);
+        // R = [h5(p4) | p5] (h6 input); backbone p5 is written into its slice 1
+        const int R = tensor(5, w[4] + w[5]);
+        View p5 = slice(R, w[4], w[5]);
+        psa("net.p5.3", full(t5c, w[5]), w[5], d[4], p5, 5);
+        // ---- DarkFPN (nn.py:192-209)
+        const int Q = tensor(4, w[3] + w[4]);   // [h3(p3) | h1 out]
+        View h1o = slice(Q, w[3], w[4]);
+        csp("fpn.h1", {Seg{p5, 1}, Seg{full(b4, w[4]), 0}}, {w[5], w[4]}, w[4], d[5], c0, 2, h1o, 4);
+        const int P3 = tensor(3, w[3]);
+        csp("fpn.h2", {Seg{h1o, 1}, Seg{full(b3, w[4]), 0}}, {w[4], w[4]}, w[3], d[5], c0, 2, full(P3, w[3]), 3);
+        conv3("fpn.h3", full(P3, w[3]), w[3], w[3], 2, ACT_SILU, slice(Q, 0, w[3]));
+        const int P4 = tensor(4, w[4]);
+        csp("fpn.h4", {Seg{full(Q), 0}}, {w[3] + w[4]}, w[4], d[5], c0, 2, full(P4, w[4]), 4);
+        conv3("fpn.h5", full(P4, w[4]), w[4], w[4], 2, ACT_SILU, slice(R, 0, w[4]));
+        const int P5 = tensor(5, w[5]);
+        csp("fpn.h6", {Seg{full(R), 0}}, {w[4] + w[5]}, w[5], d[5], c1, 2, full(P5, w[5]), 5);
+        // ---- Head (nn.py:228-270)
+        const int boxc = std::max(64, w[3] / 4);
+        const int clsc = std::max(std::max(80, w[3]), nc);
+        const int ncp = round_up(nc, 8);
+        const int xs[3] = {P3, P4, P5};
+        const int xc[3] = {w[3], w[4], w[5]};
+        int L[3];
+        for (int l = 0; l < 3; ++l) {
+            const int lvl = 3 + l;
+            L[l] = tensor(lvl, 64 + ncp);
+            const std::string bp = "head.box." + std::to_string(l);
+            const int tb1 = tensor(lvl, boxc), tb2 = tensor(lvl, boxc);
+            conv3(bp + ".0", full(xs[l], xc[l]), xc[l], boxc, 1, ACT_SILU, full(tb1, boxc));
+            conv3(bp + ".1", full(tb1, boxc), boxc, boxc, 1, ACT_SILU, full(tb2, boxc));
+            dense(bp + ".2", {Seg{full(tb2, boxc), 0}}, {boxc}, 64, 1, 1, ACT_ID, slice(L[l], 0, 64), nullptr, 1);
+        }
+        for (int l = 0; l < 3; ++l) {
+            const int lvl = 3 + l;
+            const std::string cp = "head.cls." + std::to_string(l);
+            const int tc1 = tensor(lvl, xc[l]), tc2 = tensor(lvl, clsc), tc3 = tensor(lvl, clsc), tc4 = tensor(lvl, clsc);
+            dw(cp + ".0", full(xs[l], xc[l]), xc[l], full(tc1, xc[l]));
+            conv1(cp + ".1", full(tc1, xc[l]), xc[l], clsc, ACT_SILU, full(tc2, clsc));
+            dw(cp + ".2", full(tc2, clsc), clsc, full(tc3, clsc));
+            conv1(cp + ".3", full(tc3, clsc), clsc, clsc, ACT_SILU, full(tc4, clsc));
+            View o;
+            o.t = L[l];
+            o.coff = 64;
+            o.C = ncp;
+            dense(cp + ".4", {Seg{full(tc4, clsc), 0}}, {clsc}, nc, 1, 1, ACT_ID, o, nullptr, 1);
+        }
+        Op dec;
+        dec.kind = OP_DECODE;
+        for (int l = 0; l < 3; ++l) dec.lvl[l] = full(L[l]);
+        dec.label = "head.decode";
+        ops.push_back(dec);
+        finalize_convs();
+    }
+    void dw(const std::string& name, View x, int ch, View out) {
+        const int ci = new_conv(name, CK_DW, ch, ch, 3, 1, ch, 0, ACT_SILU);
+        Op op;
+        op.kind = OP_DW;
+        op.conv = ci;
+        op.in = {Seg{x, 0}};
+        op.out = out;
+        op.label = name;
+        ops.push_back(op);
+    }
+
+    void finalize_convs() {
+        for (auto& d : convs) {
+            if (d.kind == CK_DENSE) {
+                d.cin_p = 0;
+                for (auto& s : d.segs) d.cin_p += s.second;
+                d.K = d.k * d.k * d.cin_p;
+                d.Kp = round_up(d.K, 32);
+                d.cout_p = round_up(d.cout, 8);
+                d.coutp_pad = round_up(d.cout_p, 128);
+            } else {
+                d.cin_p = round_up(d.cin, 8);
+                d.cout_p = round_up(d.cout, 8);
+                d.coutp_pad = d.cout_p;
+            }
+        }
+    }
+
+    // ---------------------------------------------------------- weights
+    void load_conv(int idx, const float* w, const float* b, const float* g, const float* be, const float* mu,
+                   const float* var_, double eps) {
+        require(idx >= 0 && idx < (int)convs.size(), "conv index out of range");
+        ConvDesc& d = convs[idx];
+        const int cpg = d.cin / d.groups;
+        const size_t per = (size_t)cpg * d.k * d.k;
+        d.wf.assign(w, w + per * d.cout);
+        d.bf.assign(d.cout, 0.0f);
+        if (b) for (int o = 0; o < d.cout; ++o) d.bf[o] = b[o];
+        if (g) {
+            // fuse_conv (nets/nn.py:8-25), fp32 throughout:
+            //   s = gamma / sqrt(eps + var); W' = s * W; b' = s * b + (beta - gamma*mean / sqrt(var + eps))
+            const float epsf = (float)eps;
+            for (int o = 0; o < d.cout; ++o) {
+                const float den = std::sqrt(var_[o] + epsf);
+                const float s = g[o] / den;
+                for (size_t i = 0; i < per; ++i) d.wf[o * per + i] = s * d.wf[o * per + i];
+                const float bnorm = be[o] - (g[o] * mu[o]) / den;
+                d.bf[o] = s * d.bf[o] + bnorm;
+            }
+        }
+        upload(d);
+        d.loaded = true;
+    }
+
+    void upload(ConvDesc& d) {
+        free_conv(d);
+        std::vector<float> bias(d.coutp_pad, 0.0f);
+        for (int o = 0; o < d.cout; ++o) bias[o] = d.bf[o];
+        HIPCHECK(hipMalloc(&d.b_dev, bias.size() * 4));
+        HIPCHECK(hipMemcpy(d.b_dev, bias.data(), bias.size() * 4, hipMemcpyHostToDevice));
+        if (d.kind == CK_DENSE) {
+            // packed [coutp_pad][Kp], k = (kh*KW + kw)*cin_p + ci_phys
+            std::vector<float> wp((size_t)d.coutp_pad * d.Kp, 0.0f);
+            std::vector<int> ktab(d.Kp / 8, 0xffff);
+            // physical -> logical channel map
+            std::vector<int> phys2log(d.cin_p, -1);
+            int lo = 0, ph = 0;
+            for (auto& s : d.segs) {
+                for (int c = 0; c < s.first; ++c) phys2log[ph + c] = lo + c;
+                lo += s.first;
+                ph += s.second;
+            }
+            const size_t per = (size_t)d.cin * d.k * d.k;
+            for (int kh = 0; kh < d.k; ++kh)
+                for (int kw = 0; kw < d.k; ++kw)
+                    for (int cp = 0; cp < d.cin_p; ++cp) {
+                        const int kk = (kh * d.k + kw) * d.cin_p + cp;
+                        if (cp % 8 == 0) ktab[kk / 8] = (kh << 24) | (kw << 16) | cp;
+                        const int cl = phys2log[cp];
+                        if (cl < 0) continue;
+                        for (int o = 0; o < d.cout; ++o)
+                            wp[(size_t)o * d.Kp + kk] = d.wf[o * per + (size_t)cl * d.k * d.k + kh * d.k + kw];
+                    }
+            d.w_dev = to_device(wp);
+            HIPCHECK(hipMalloc(&d.ktab_dev, ktab.size() * 4));
+            HIPCHECK(hipMemcpy(d.ktab_dev, ktab.data(), ktab.size() * 4, hipMemcpyHostToDevice));
+        } else if (d.kind == CK_FIRST) {
+            // transposed [27][cout_p]: k = ci*9 + kh*3 + kw
+            std::vector<float> wp((size_t)d.cout_p * 27, 0.0f);
+            for (int o = 0; o < d.cout; ++o)
+                for (int k = 0; k < 27; ++k) wp[(size_t)k * d.cout_p + o] = d.wf[(size_t)o * 27 + k];
+            HIPCHECK(hipMalloc(&d.w_dev, wp.size() * 4));
+            HIPCHECK(hipMemcpy(d.w_dev, wp.data(), wp.size() * 4, hipMemcpyHostToDevice));
+        } else {  // depthwise / pe: [9][C] fp32
+            std::vector<float> wp((size_t)9 * d.cout_p, 0.0f);
+            for (int c = 0; c < d.cout; ++c)
+                for (int t = 0; t < 9; ++t) wp[(size_t)t * d.cout_p + c] = d.wf[(size_t)c * 9 + t];
+            HIPCHECK(hipMalloc(&d.w_dev, wp.size() * 4));
+            HIPCHECK(hipMemcpy(d.w_dev, wp.data(), wp.size() * 4, hipMemcpyHostToDevice));
+        }
+    }
+
+    void* to_device(const std::vector<float>& v) {
+        void* p = nullptr;
+        if (dtype == F32) {
+            HIPCHECK(hipMalloc(&p, v.size() * 4));
+            HIPCHECK(hipMemcpy(p, v.data(), v.size() * 4, hipMemcpyHostToDevice));
+        } else {
+            std::vector<uint16_t> h(v.size());
+            for (size_t i = 0; i < v.size(); ++i) h[i] = dtype == BF16 ? f2bf(v[i]) : f2h(v[i]);
+            HIPCHECK(hipMalloc(&p, h.size() * 2));
+            HIPCHECK(hipMemcpy(p, h.data(), h.size() * 2, hipMemcpyHostToDevice));
+        }
+        return p;
+    }
+
+    static void free_conv(ConvDesc& d) {
+        if (d.w_dev) (void)hipFree(d.w_dev);
+        if (d.b_dev) (void)hipFree(d.b_dev);
+        if (d.ktab_dev) (void)hipFree(d.ktab_dev);
+        d.w_dev = nullptr;
+        d.b_dev = nullptr;
+        d.ktab_dev = nullptr;
+    }
+
+    // ---------------------------------------------------------- workspace
+    size_t ws_bytes_for(int B, int H, int W, std::vector<size_t>* offs) const {
+        size_t total = 0;
+        if (offs) offs->assign(tensors.size(), 0);
+        for (size_t i = 0; i < tensors.size(); ++i) {
+            const Tensor& t = tensors[i];
+            const size_t b = (size_t)B * (H >> t.level) * (W >> t.level) * t.C * es;
+            if (offs) (*offs)[i] = total;
+            total += (b + 255) & ~(size_t)255;
+        }
+        return total;
+    }
+    void reserve(int B, int H, int W) {
+        require(B > 0 && H > 0 && W > 0 && H % 32 == 0 && W % 32 == 0, "input height/width must be positive multiples of 32");
+        if (ws.base && ws.B == B && ws.H == H && ws.W == W) return;
+        std::vector<size_t> offs;
+        const size_t need = ws_bytes_for(B, H, W, &offs);
+        if (!ws.base || need > ws.bytes) {
+            drop_graphs();
+            if (ws.base) HIPCHECK(hipFree(ws.base));
+            ws.base = nullptr;
+            const hipError_t e = hipMalloc(&ws.base, need);
+            if (e != hipSuccess) throw Fail(YH_ENOMEM, "workspace allocation failed");
+            ws.bytes = need;
+        } else if (ws.B != B || ws.H != H || ws.W != W) {
+            drop_graphs();
+        }
+        ws.off = offs;
+        ws.B = B;
+        ws.H = H;
+        ws.W = W;
+    }
+    char* ptr(const View& v) const {
+        return (char*)ws.base + ws.off[v.t] + (size_t)v.coff * es;
+    }
+    int ldc(const View& v) const { return tensors[v.t].C; }
+
+    void drop_graphs() {
+        for (auto& kv : graphs) (void)hipGraphExecDestroy(kv.second);
+        graphs.clear();
+    }
+
+    // ---------------------------------------------------------- launches
+    static void pick_tile(long long M, int cout, int& BM, int& BN) {
+        BN = cout <= 16 ? 16 : cout <= 32 ? 32 : cout <= 64 ? 64 : 128;
+        const long long gn = (cout + BN - 1) / BN;
+        BM = 64;
+        for (int bm : {256, 128}) {
+            if (((M + bm - 1) / bm) * gn >= 1024) { BM = bm; break; }
+        }
+    }
+
+    void launch_op(size_t oi, int B, int H, int W, hipStream_t s) {
+        const Op& op = ops[oi];
+        int rc = 0;
+        switch (op.kind) {
+            case OP_FIRST: {
+                const ConvDesc& d = convs[op.conv];
+                FirstConvArgs a{};
+                a.io = (const void* const*)io_dev;
+                a.H = H; a.W = W; a.Ho = H >> 1; a.Wo = W >> 1;
+                a.Cout = d.cout_p;
+                a.ldo = ldc(op.out);
+                a.M = B * a.Ho * a.Wo;
+                a.w = (const float*)d.w_dev;
+                a.bias = d.b_dev;
+                a.out = ptr(op.out);
+                a.act = d.act;
+                rc = launch_first_conv(dtype, a, B, s);
+                break;
+            }
+            case OP_CONV: {
+                const ConvDesc& d = convs[op.conv];
+                const Tensor& to = tensors[op.out.t];
+                ConvArgs a{};
+                const int lvl_in = tensors[op.in[0].v.t].level - op.in[0].up;
+                a.Hi = H >> lvl_in; a.Wi = W >> lvl_in;
+                a.Ho = H >> to.level; a.Wo = W >> to.level;
+                a.stride = d.stride; a.pad = d.k / 2; a.KH = d.k; a.KW = d.k;
+                for (size_t si = 0; si < op.in.size(); ++si) {
+                    const Seg& sg = op.in[si];
+                    const Tensor& ts = tensors[sg.v.t];
+                    const int hh = H >> ts.level, ww = W >> ts.level;
+                    if (si == 0) { a.in0 = ptr(sg.v); a.ldc0 = ts.C; a.c0 = sg.v.C; a.up0 = sg.up; a.h0 = hh; a.w0 = ww; }
+                    else { a.in1 = ptr(sg.v); a.ldc1 = ts.C; a.c1 = sg.v.C; a.up1 = sg.up; a.h1 = hh; a.w1 = ww; }
+                }
+                if (op.in.size() == 1) { a.in1 = a.in0; a.ldc1 = a.ldc0; a.c1 = 0; a.up1 = 0; a.h1 = a.h0; a.w1 = a.w0; }
+                a.Cin = d.cin_p; a.K = d.K; a.Kp = d.Kp;
+                a.M = B * a.Ho * a.Wo;
+                a.w = d.w_dev; a.bias = d.b_dev; a.ktab = d.ktab_dev;
+                a.out = ptr(op.out); a.ldo = to.C;
+                if (op.has_res) { a.res = ptr(op.res); a.ldr = ldc(op.res); }
+                a.Cout = d.cout_p;
+                a.act = d.act;
+                int BM, BN;
+                pick_tile(a.M, a.Cout, BM, BN);
+                a.gm = (a.M + BM - 1) / BM;
+                a.gn = (a.Cout + BN - 1) / BN;
+                rc = launch_conv(dtype, BM, BN, a, s);
+                break;
+            }
+            case OP_DW: {
+                const ConvDesc& d = convs[op.conv];
+                const Tensor& ti = tensors[op.in[0].v.t];
+                DwArgs a{};
+                a.in = ptr(op.in[0].v); a.ldi = ti.C;
+                a.H = H >> ti.level; a.W = W >> ti.level; a.C = d.cout_p; a.M = B * a.H * a.W;
+                a.w = (const float*)d.w_dev; a.bias = d.b_dev;
+                a.out = ptr(op.out); a.ldo = ldc(op.out); a.act = d.act;
+                rc = launch_dwconv(dtype, a, s);
+                break;
+            }
+            case OP_SPPF: {
+                const Tensor& t = tensors[op.out.t];
+                PoolArgs a{};
+                a.buf = ptr(op.out); a.ldc = t.C; a.C = op.out.C; a.H = H >> t.level; a.W = W >> t.level; a.B = B;
+                rc = launch_sppf(dtype, a, s);
+                break;
+            }
+            case OP_ATTN: {
+                const ConvDesc& d = convs[op.conv];
+                const Tensor& tq = tensors[op.in[0].v.t];
+                AttnArgs a{};
+                a.qkv = ptr(op.in[0].v); a.ldq = tq.C;
+                a.Hs = H >> tq.level; a.Ws = W >> tq.level; a.T = a.Hs * a.Ws;
+                a.heads = op.heads; a.dk = 32; a.dh = 64;
+                a.scale = (float)std::pow(32.0, -0.5);
+                a.pe_w = (const float*)d.w_dev; a.pe_b = d.b_dev;
+                a.out = ptr(op.out); a.ldo = ldc(op.out);
+                rc = launch_attention(dtype, a, B, s);
+                break;
+            }
+            case OP_DECODE: {
+                DecodeArgs a{};
+                for (int l = 0; l < 3; ++l) {
+                    const Tensor& t = tensors[op.lvl[l].t];
+                    a.lvl[l] = ptr(op.lvl[l]);
+                    a.H[l] = H >> t.level; a.W[l] = W >> t.level;
+                    a.stride[l] = (float)(1 << t.level);
+                    a.ldc = t.C;
+                }
+                a.nc = var.num_classes;
+                a.A = a.H[0] * a.W[0] + a.H[1] * a.W[1] + a.H[2] * a.W[2];
+                a.B = B;
+                a.io = (const void* const*)io_dev;
+                rc = launch_decode(dtype, a, s);
+                break;
+            }
+        }
+        if (rc != 0) throw Fail(YH_EHIP, "launch of " + op.label + " failed: " + hipGetErrorString((hipError_t)rc));
+    }
+
+    void run_ops(int B, int H, int W, hipStream_t s) {
+        for (size_t i = 0; i < ops.size(); ++i) launch_op(i, B, H, W, s);
+    }
+
+    void forward(const void* x, int B, int H, int W, void* y, hipStream_t s) {
+        for (auto& d : convs) require(d.loaded, "weights of " + d.name + " not loaded", YH_ESTATE);
+        reserve(B, H, W);
+        HIPCHECK(hipSetDevice(device));
+        require(launch_set_io(io_dev, x, y, s) == 0, "set_io launch failed", YH_EHIP);
+        lastB = B; lastH = H; lastW = W;
+        if (profile) {
+            if (ev.size() < 2 * ops.size()) {
+                for (auto e : ev) (void)hipEventDestroy(e);
+                ev.assign(2 * ops.size(), nullptr);
+                for (auto& e : ev) HIPCHECK(hipEventCreate(&e));
+            }
+            prof_ms.resize(ops.size(), 0.0);
+            prof_calls.resize(ops.size(), 0);
+            for (size_t i = 0; i < ops.size(); ++i) {
+                HIPCHECK(hipEventRecord(ev[2 * i], s));
+                launch_op(i, B, H, W, s);
+                HIPCHECK(hipEventRecord(ev[2 * i + 1], s));
+            }
+            HIPCHECK(hipEventSynchronize(ev[2 * ops.size() - 1]));
+            for (size_t i = 0; i < ops.size(); ++i) {
+                float ms = 0.f;
+                HIPCHECK(hipEventElapsedTime(&ms, ev[2 * i], ev[2 * i + 1]));
+                prof_ms[i] += ms;
+                prof_calls[i] += 1;
+            }
+            return;
+        }
+        if (!use_graph) {
+            run_ops(B, H, W, s);
+            return;
+        }
+        const GraphKey key{B, H, W};
+        auto it = graphs.find(key);
+        if (it == graphs.end()) {
+            if (!cap_stream) HIPCHECK(hipStreamCreateWithFlags(&cap_stream, hipStreamNonBlocking));
+            hipGraph_t g = nullptr;
+            HIPCHECK(hipStreamBeginCapture(cap_stream, hipStreamCaptureModeThreadLocal));
+            try {
+                run_ops(B, H, W, cap_stream);
+            } catch (...) {
+                (void)hipStreamEndCapture(cap_stream, &g);
+                if (g) (void)hipGraphDestroy(g);
+                throw;
+            }
+            HIPCHECK(hipStreamEndCapture(cap_stream, &g));
+            hipGraphExec_t ex = nullptr;
+            HIPCHECK(hipGraphInstantiate(&ex, g, nullptr, nullptr, 0));
+            (void)hipGraphDestroy(g);
+            it = graphs.emplace(key, ex).first;
+        }
+        HIPCHECK(hipGraphLaunch(it->second, s));
+    }
+
+    // ---------------------------------------------------------- per-op accounting
+    OpClass op_class(const Op& op) const {
+        switch (op.kind) {
+            case OP_FIRST: return CL_FIRST;
+            case OP_CONV: return convs[op.conv].k == 3 ? CL_CONV3 : CL_CONV1;
+            case OP_DW: return CL_DW;
+            case OP_SPPF: return CL_SPPF;
+            case OP_ATTN: return CL_ATTN;
+            case OP_DECODE: return CL_DECODE;
+        }
+        return CL_CONV1;
+    }
+    // algorithmic bytes (each operand read once, output written once) and flops per call
+    void op_cost(const Op& op, int B, int H, int W, double& bytes, double& flops) const {
+        bytes = 0; flops = 0;
+        auto px = [&](int level) { return (double)B * (H >> level) * (W >> level); };
+        switch (op.kind) {
+            case OP_FIRST: {
+                const ConvDesc& d = convs[op.conv];
+                const double out = px(1);
+                bytes = (double)B * 3 * H * W * es + out * d.cout * es + d.cout * 27.0 * 4;
+                flops = 2.0 * out * d.cout * 27;
+                break;
+            }
+            case OP_CONV: {
+                const ConvDesc& d = convs[op.conv];
+                const double out = px(tensors[op.out.t].level);
+                for (size_t si = 0; si < op.in.size(); ++si) {
+                    const Seg& sg = op.in[si];
+                    bytes += px(tensors[sg.v.t].level) * d.segs[si].first * es;
+                }
+                bytes += out * d.cout * es + (double)d.cout * d.cin * d.k * d.k * es;
+                if (op.has_res) bytes += out * d.cout * es;
+                flops = 2.0 * out * d.cout * d.cin * d.k * d.k;
+                break;
+            }
+            case OP_DW: {
+                const ConvDesc& d = convs[op.conv];
+                const double n = px(tensors[op.out.t].level);
+                bytes = 2.0 * n * d.cout * es;
+                flops = 2.0 * n * d.cout * 9;
+                break;
+            }
+            case OP_SPPF: {
+                const double n = px(tensors[op.out.t].level);
+                bytes = 6.0 * n * op.out.C * es;
+                flops = 3.0 * n * op.out.C * 25;
+                break;
+            }
+            case OP_ATTN: {
+                const double T = (double)(H >> tensors[op.out.t].level) * (W >> tensors[op.out.t].level);
+                const double C = op.heads * 64.0;
+                bytes = (double)B * T * (op.heads * 128.0 + C) * es;
+                flops = (double)B * op.heads * (2.0 * T * T * (32 + 64)) + 2.0 * B * T * C * 9;
+                break;
+            }
+            case OP_DECODE: {
+                double A = 0, cin = 0;
+                for (int l = 0; l < 3; ++l) {
+                    A += px(tensors[op.lvl[l].t].level);
+                    cin = tensors[op.lvl[l].t].C;
+                }
+                bytes = A * (64 + var.num_classes) * es + A * (4 + var.num_classes) * es;
+                (void)cin;
+                flops = A * (64 * 4.0 + var.num_classes * 4.0);
+                break;
+            }
+        }
+    }
+
+    ~Net() {
+        drop_graphs();
+        for (auto& d : convs) free_conv(d);
+        if (ws.base) (void)hipFree(ws.base);
+        if (io_dev) (void)hipFree(io_dev);
+        if (cap_stream) (void)hipStreamDestroy(cap_stream);
+        for (auto e : ev) (void)hipEventDestroy(e);
+    }
+};
+
+}  // namespace yh
+
+struct yh_handle {
+    yh::Net net;
+};
+
+using yh::Fail;
+
+namespace {
+
+template <typename F>
+int guarded(F&& f) {
+    try {
+        f();
+        yh::g_err.clear();
+        return YH_OK;
+    } catch (const Fail& e) {
+        yh::g_err = e.what();
+        return e.code;
+    } catch (const std::exception& e) {
+        yh::g_err = e.what();
+        return YH_EINVAL;
+    } catch (...) {
+        yh::g_err = "unknown error";
+        return YH_EINVAL;
+    }
+}
+
+}  // namespace
+
+extern "C" {
+
+int yh_abi_version(void) { return YH_ABI_VERSION; }
+
+const char* yh_last_error(void) { return yh::g_err.c_str(); }
+
+int yh_create(const yh_variant* v, int device, int dtype, yh_handle** out) {
+    return guarded([&] {
+        yh::require(v && out, "null argument");
+        yh::require(dtype == YH_F32 || dtype == YH_F16 || dtype == YH_BF16, "dtype must be YH_F32, YH_F16 or YH_BF16");
+        yh::require(v->num_classes > 0, "num_classes must be positive");
+        for (int i = 1; i < 6; ++i) yh::require(v->width[i] > 0 && v->width[i] % 8 == 0, "widths must be multiples of 8");
+        yh::require(v->width[0] == 3, "input channels (width[0]) must be 3");
+        for (int i = 0; i < 6; ++i) yh::require(v->depth[i] >= 1, "depths must be >= 1");
+        int ndev = 0;
+        HIPCHECK(hipGetDeviceCount(&ndev));
+        yh::require(device >= 0 && device < ndev, "device ordinal out of range");
+        HIPCHECK(hipSetDevice(device));
+        std::unique_ptr<yh_handle> h(new yh_handle());
+        yh::Net& n = h->net;
+        n.var = *v;
+        n.device = device;
+        n.dtype = dtype;
+        n.es = yh::dtype_size(dtype);
+        n.build();
+        HIPCHECK(hipMalloc(&n.io_dev, 2 * sizeof(void*)));
+        *out = h.release();
+    });
+}
+
+void yh_destroy(yh_handle* h) {
+    if (!h) return;
+    (void)hipSetDevice(h->net.device);
+    delete h;
+}
+
+int yh_conv_count(const yh_handle* h) { return h ? (int)h->net.convs.size() : YH_EINVAL; }
+
+int yh_conv_info(const yh_handle* h, int index, const char** name, int* cout, int* cin_per_group, int* ksize,
+                 int* groups, int* has_bias) {
+    return guarded([&] {
+        yh::require(h && index >= 0 && index < (int)h->net.convs.size(), "conv index out of range");
+        const yh::ConvDesc& d = h->net.convs[index];
+        if (name) *name = d.name.c_str();
+        if (cout) *cout = d.cout;
+        if (cin_per_group) *cin_per_group = d.cin / d.groups;
+        if (ksize) *ksize = d.k;
+        if (groups) *groups = d.groups;
+        if (has_bias) *has_bias = d.has_bias;
+    });
+}
+
+int yh_load_conv(yh_handle* h, int index, const float* weight, const float* bias, const float* bn_gamma,
+                 const float* bn_beta, const float* bn_mean, const float* bn_var, double bn_eps) {
+    return guarded([&] {
+        yh::require(h && weight, "null argument");
+        yh::require(!bn_gamma || (bn_beta && bn_mean && bn_var), "BatchNorm needs gamma, beta, mean and var");
+        HIPCHECK(hipSetDevice(h->net.device));
+        h->net.load_conv(index, weight, bias, bn_gamma, bn_beta, bn_mean, bn_var, bn_eps);
+    });
+}
+
+int yh_num_anchors(const yh_handle* h, int height, int width, int* anchors) {
+    return guarded([&] {
+        yh::require(h && anchors, "null argument");
+        yh::require(height > 0 && width > 0 && height % 32 == 0 && width % 32 == 0, "height/width must be multiples of 32");
+        int a = 0;
+        for (int l = 3; l <= 5; ++l) a += (height >> l) * (width >> l);
+        *anchors = a;
+    });
+}
+
+int yh_workspace_bytes(const yh_handle* h, int batch, int height, int width, size_t* bytes) {
+    return guarded([&] {
+        yh::require(h && bytes, "null argument");
+        yh::require(batch > 0 && height % 32 == 0 && width % 32 == 0, "bad shape");
+        *bytes = h->net.ws_bytes_for(batch, height, width, nullptr);
+    });
+}
+
+int yh_reserve(yh_handle* h, int batch, int height, int width) {
+    return guarded([&] {
+        yh::require(h, "null handle");
+        HIPCHECK(hipSetDevice(h->net.device));
+        h->net.reserve(batch, height, width);
+    });
+}
+
+int yh_forward(yh_handle* h, const void* x, int batch, int height, int width, void* y, void* stream) {
+    return guarded([&] {
+        yh::require(h && x && y, "null argument");
+        yh::require(batch > 0, "batch must be positive");
+        HIPCHECK(hipSetDevice(h->net.device));
+        h->net.forward(x, batch, height, width, y, (hipStream_t)stream);
+    });
+}
+
+size_t yh_nms_workspace_bytes(int batch, int num_classes, int anchors) {
+    if (batch <= 0 || num_classes <= 0 || anchors <= 0) return 0;
+    return (size_t)batch * anchors * num_classes * 8 + (size_t)batch * 4 + 256;
+}
+
+int yh_nms(int dtype, const void* y, int batch, int num_classes, int anchors, float conf_threshold,
+           double iou_threshold, int max_det, int max_nms, float max_wh, void* workspace, size_t workspace_bytes,
+           float* dets, int* counts, void* stream) {
+    return guarded([&] {
+        yh::require(y && dets && counts && workspace, "null argument");
+        yh::require(dtype == YH_F32 || dtype == YH_F16 || dtype == YH_BF16, "bad dtype");
+        yh::require(batch > 0 && anchors > 0 && num_classes > 0, "bad shape");
+        yh::require(max_det > 0 && max_det <= 1024, "max_det must be in [1, 1024]");
+        yh::require(max_nms > 0, "max_nms must be positive");
+        yh::require(conf_threshold >= 0.0f, "conf_threshold must be >= 0");
+        yh::require((long long)anchors * num_classes < (1ll << 26), "anchors * classes exceeds 2^26");
+        yh::require(workspace_bytes >= yh_nms_workspace_bytes(batch, num_classes, anchors), "NMS workspace too small");
+        yh::NmsArgs a{};
+        a.y = y; a.B = batch; a.A = anchors; a.nc = num_classes;
+        // compare in the input dtype: torch rounds the Python-float threshold to
+        // the tensor dtype before comparing (util.py:130,147)
+        float conf = conf_threshold;
+        if (dtype == YH_F16) {
+            const uint16_t hb = yh::f2h(conf);
+            const uint32_t ex = (hb >> 10) & 0x1f, mt = hb & 0x3ff;
+            conf = ex == 0 ? std::ldexp((float)mt, -24)
+                 : ex == 31 ? INFINITY : std::ldexp((float)(mt | 0x400), (int)ex - 25);
+        } else if (dtype == YH_BF16) {
+            const uint32_t u = (uint32_t)yh::f2bf(conf) << 16;
+            std::memcpy(&conf, &u, 4);
+        }
+        a.conf = conf;
+        // largest float <= iou_threshold: for any float ovr, ovr > thr (double) <=> ovr > a.iou
+        float t = (float)iou_threshold;
+        if ((double)t > iou_threshold) t = std::nextafter(t, -INFINITY);
+        a.iou = t;
+        a.max_wh = max_wh;
+        a.max_det = max_det;
+        a.max_nms = max_nms;
+        a.keys = (unsigned long long*)workspace;
+        a.counts = (int*)((char*)workspace + (size_t)batch * anchors * num_classes * 8);
+        a.dets = dets;
+        a.ndet = counts;
+        const int rc = yh::launch_nms(dtype, a, (hipStream_t)stream);
+        if (rc != 0) throw Fail(YH_EHIP, std::string("NMS launch failed: ") + hipGetErrorString((hipError_t)rc));
+    });
+}
+
+int yh_set_graph(yh_handle* h, int enable) {
+    return guarded([&] {
+        yh::require(h, "null handle");
+        h->net.use_graph = enable != 0;
+    });
+}
+
+int yh_profile_enable(yh_handle* h, int enable) {
+    return guarded([&] {
+        yh::require(h, "null handle");
+        h->net.profile = enable != 0;
+    });
+}
+
+int yh_profile_reset(yh_handle* h) {
+    return guarded([&] {
+        yh::require(h, "null handle");
+        std::fill(h->net.prof_ms.begin(), h->net.prof_ms.end(), 0.0);
+        std::fill(h->net.prof_calls.begin(), h->net.prof_calls.end(), 0);
+    });
+}
+
+int yh_op_count(const yh_handle* h) { return h ? (int)h->net.ops.size() : YH_EINVAL; }
+
+int yh_op_info(const yh_handle* h, int index, int batch, int height, int width, const char** label, int* op_class,
+               double* bytes, double* flops, double* ms_total, int* calls) {
+    return guarded([&] {
+        yh::require(h && index >= 0 && index < (int)h->net.ops.size(), "op index out of range");
+        const yh::Net& n = h->net;
+        const yh::Op& op = n.ops[index];
+        if (label) *label = op.label.c_str();
+        if (op_class) *op_class = (int)n.op_class(op);
+        double b = 0, f = 0;
+        n.op_cost(op, batch, height, width, b, f);
+        if (bytes) *bytes = b;
+        if (flops) *flops = f;
+        if (ms_total) *ms_total = index < (int)n.prof_ms.size() ? n.prof_ms[index] : 0.0;
+        if (calls) *calls = index < (int)n.prof_calls.size() ? n.prof_calls[index] : 0;
+    });
+}
+
+}  // extern "C"

@@ -1,0 +1,281 @@
+// Non-GEMM kernels of the forward:
+//   maxpool5    SPPF's three chained 5x5/s1/p2 max-pools (nets/nn.py:83-94)
+//   psa_attention  C2PSA attention (nets/nn.py:111-123) with the positional
+//               depthwise conv pe(v) fused into its epilogue
+//   head_decode DFL + anchors + dist2bbox + sigmoid (nets/nn.py:255-270,
+//               222-225; utils/util.py:85-96) into the caller's (B, 4+nc, A)
+//   set_io      publishes the caller's x / y pointers for graph replay
+#include "common.h"
+#include "dtypes.h"
+
+namespace yh {
+
+namespace {
+
+template <typename T> __device__ __forceinline__ float ex(float x) { return __expf(x); }
+template <> __device__ __forceinline__ float ex<float>(float x) { return expf(x); }
+
+template <typename T>
+__global__ __launch_bounds__(256) void maxpool5(const T* src, T* dst, int ldc, int C, int H, int W, int M) {
+    // One thread = one pixel x 8 channels; -inf padding == skip out-of-range taps.
+    const int cpp = C / 8;
+    const long long idx = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= (long long)M * cpp) return;
+    const int m = (int)(idx / cpp), cc = (int)(idx - (long long)m * cpp);
+    const int HW = H * W;
+    const int n = m / HW, r = m - n * HW;
+    const int h = r / W, w = r - h * W;
+    const T* base = src + (long long)n * HW * ldc + cc * 8;
+    float mx[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) mx[e] = -INFINITY;
+    for (int dh = -2; dh <= 2; ++dh) {
+        const int hi = h + dh;
+        if (hi < 0 || hi >= H) continue;
+        for (int dw = -2; dw <= 2; ++dw) {
+            const int wi = w + dw;
+            if (wi < 0 || wi >= W) continue;
+            float f[8];
+            chunk_to_f(ld_chunk(base + ((long long)hi * W + wi) * ldc), f);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) mx[e] = fmaxf(mx[e], f[e]);
+        }
+    }
+    st_chunk(dst + (long long)m * ldc + cc * 8, f_to_chunk<T>(mx));
+}
+
+template <typename T>
+int launch_sppf_t(const PoolArgs& a, hipStream_t s) {
+    T* b = reinterpret_cast<T*>(a.buf);
+    const int M = a.B * a.H * a.W;
+    const long long n = (long long)M * (a.C / 8);
+    const dim3 g((unsigned)((n + 255) / 256));
+    for (int i = 0; i < 3; ++i) {
+        hipLaunchKernelGGL((maxpool5<T>), g, dim3(256), 0, s, b + i * a.C, b + (i + 1) * a.C, a.ldc, a.C, a.H, a.W, M);
+    }
+    return (int)hipGetLastError();
+}
+
+constexpr int ATT_Q = 64;   // queries per block (one wave, one query per lane)
+constexpr int ATT_KB = 64;  // keys staged per LDS tile
+constexpr int DK = 32, DH = 64;
+
+template <typename T>
+__global__ __launch_bounds__(ATT_Q) void psa_attention(const AttnArgs p) {
+    __shared__ float ks[ATT_KB][DK];
+    __shared__ float vs[ATT_KB][DH];
+    const int qi = blockIdx.x * ATT_Q + threadIdx.x;
+    const int head = blockIdx.y, n = blockIdx.z;
+    const int per = 2 * DK + DH;
+    const T* base = reinterpret_cast<const T*>(p.qkv) + (long long)n * p.T * p.ldq + head * per;
+    const bool live = qi < p.T;
+
+    float q[DK];
+    if (live) {
+#pragma unroll
+        for (int c = 0; c < DK; c += 8) {
+            float f[8];
+            chunk_to_f(ld_chunk(base + (long long)qi * p.ldq + c), f);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) q[c + e] = f[e];
+        }
+    } else {
+#pragma unroll
+        for (int c = 0; c < DK; ++c) q[c] = 0.f;
+    }
+    float acc[DH];
+#pragma unroll
+    for (int d = 0; d < DH; ++d) acc[d] = 0.f;
+    float mrun = -INFINITY, lrun = 0.f;
+
+    for (int kb = 0; kb < p.T; kb += ATT_KB) {
+        const int nk = min(ATT_KB, p.T - kb);
+        __syncthreads();
+        if ((int)threadIdx.x < nk) {
+            const T* row = base + (long long)(kb + threadIdx.x) * p.ldq;
+#pragma unroll
+            for (int c = 0; c < DK; c += 8) {
+                float f[8];
+                chunk_to_f(ld_chunk(row + DK + c), f);
+#pragma unroll
+                for (int e = 0; e < 8; ++e) ks[threadIdx.x][c + e] = f[e];
+            }
+#pragma unroll
+            for (int c = 0; c < DH; c += 8) {
+                float f[8];
+                chunk_to_f(ld_chunk(row + 2 * DK + c), f);
+#pragma unroll
+                for (int e = 0; e < 8; ++e) vs[threadIdx.x][c + e] = f[e];
+            }
+        }
+        __syncthreads();
+        float s[ATT_KB];
+        float mx = -INFINITY;
+#pragma unroll
+        for (int j = 0; j < ATT_KB; ++j) {
+            float d = 0.f;
+#pragma unroll
+            for (int c = 0; c < DK; ++c) d = fmaf(q[c], ks[j][c], d);
+            d = (j < nk) ? d * p.scale : -INFINITY;
+            s[j] = d;
+            mx = fmaxf(mx, d);
+        }
+        const float mnew = fmaxf(mrun, mx);
+        const float corr = ex<T>(mrun - mnew);
+        lrun *= corr;
+#pragma unroll
+        for (int d = 0; d < DH; ++d) acc[d] *= corr;
+#pragma unroll
+        for (int j = 0; j < ATT_KB; ++j) {
+            const float pj = (j < nk) ? ex<T>(s[j] - mnew) : 0.f;
+            lrun += pj;
+#pragma unroll
+            for (int d = 0; d < DH; ++d) acc[d] = fmaf(pj, vs[j][d], acc[d]);
+        }
+        mrun = mnew;
+    }
+    if (!live) return;
+
+    // epilogue: normalise, add pe(v) = depthwise 3x3 over v (+ bias), store.
+    const float inv = 1.0f / lrun;
+    const int hq = qi / p.Ws, wq = qi - hq * p.Ws;
+    const int C = p.heads * DH;
+    float o[DH];
+#pragma unroll
+    for (int d = 0; d < DH; ++d) o[d] = acc[d] * inv + p.pe_b[head * DH + d];
+    for (int kh = 0; kh < 3; ++kh) {
+        const int hi = hq - 1 + kh;
+        if (hi < 0 || hi >= p.Hs) continue;
+        for (int kw = 0; kw < 3; ++kw) {
+            const int wi = wq - 1 + kw;
+            if (wi < 0 || wi >= p.Ws) continue;
+            const T* v = base + (long long)(hi * p.Ws + wi) * p.ldq + 2 * DK;
+            const float* wt = p.pe_w + (kh * 3 + kw) * C + head * DH;
+#pragma unroll
+            for (int c = 0; c < DH; c += 8) {
+                float f[8];
+                chunk_to_f(ld_chunk(v + c), f);
+#pragma unroll
+                for (int e = 0; e < 8; ++e) o[c + e] = fmaf(wt[c + e], f[e], o[c + e]);
+            }
+        }
+    }
+    T* out = reinterpret_cast<T*>(p.out) + ((long long)n * p.T + qi) * p.ldo + head * DH;
+#pragma unroll
+    for (int c = 0; c < DH; c += 8) {
+        float f[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) f[e] = o[c + e];
+        st_chunk(out + c, f_to_chunk<T>(f));
+    }
+}
+
+template <typename T>
+int launch_attention_t(const AttnArgs& a, int B, hipStream_t s) {
+    if (a.dk != DK || a.dh != DH) return (int)hipErrorInvalidValue;
+    const dim3 g((a.T + ATT_Q - 1) / ATT_Q, a.heads, B);
+    hipLaunchKernelGGL((psa_attention<T>), g, dim3(ATT_Q), 0, s, a);
+    return (int)hipGetLastError();
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void head_decode(const DecodeArgs p) {
+    const long long idx = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= (long long)p.B * p.A) return;
+    const int n = (int)(idx / p.A), a = (int)(idx - (long long)n * p.A);
+    int l = 0, loc = a;
+    const int a0 = p.H[0] * p.W[0], a1 = p.H[1] * p.W[1];
+    if (loc >= a0) { loc -= a0; l = 1; if (loc >= a1) { loc -= a1; l = 2; } }
+    const int H = p.H[l], W = p.W[l];
+    const int gy = loc / W, gx = loc - gy * W;
+    const T* src = reinterpret_cast<const T*>(p.lvl[l]) + ((long long)n * H * W + loc) * p.ldc;
+
+    // DFL: softmax over 16 bins per side, expectation with weights 0..15.
+    float dist[4];
+#pragma unroll
+    for (int sd = 0; sd < 4; ++sd) {
+        float v[16];
+#pragma unroll
+        for (int c = 0; c < 16; c += 8) {
+            float f[8];
+            chunk_to_f(ld_chunk(src + sd * 16 + c), f);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) v[c + e] = f[e];
+        }
+        float mx = v[0];
+#pragma unroll
+        for (int i = 1; i < 16; ++i) mx = fmaxf(mx, v[i]);
+        float sum = 0.f;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) { v[i] = ex<T>(v[i] - mx); sum += v[i]; }
+        float d = 0.f;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) d = fmaf((float)i, v[i] / sum, d);
+        dist[sd] = d;
+    }
+    const float ax = (float)gx + 0.5f, ay = (float)gy + 0.5f, st = p.stride[l];
+    const float x1 = ax - dist[0], y1 = ay - dist[1];
+    const float x2 = ax + dist[2], y2 = ay + dist[3];
+    T* y = reinterpret_cast<T*>(const_cast<void*>(p.io[1])) + (long long)n * (4 + p.nc) * p.A + a;
+    y[0] = fromf<T>((x1 + x2) / 2.0f * st);
+    y[(long long)p.A] = fromf<T>((y1 + y2) / 2.0f * st);
+    y[2LL * p.A] = fromf<T>((x2 - x1) * st);
+    y[3LL * p.A] = fromf<T>((y2 - y1) * st);
+    const T* cls = src + 64;
+    for (int c = 0; c < p.nc; c += 8) {
+        float f[8];
+        chunk_to_f(ld_chunk(cls + c), f);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+            if (c + e < p.nc) y[(long long)(4 + c + e) * p.A] = fromf<T>(1.0f / (1.0f + ex<T>(-f[e])));
+        }
+    }
+}
+
+template <typename T>
+int launch_decode_t(const DecodeArgs& a, hipStream_t s) {
+    const long long n = (long long)a.B * a.A;
+    hipLaunchKernelGGL((head_decode<T>), dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, a);
+    return (int)hipGetLastError();
+}
+
+__global__ void set_io(void** io, const void* x, void* y) {
+    io[0] = const_cast<void*>(x);
+    io[1] = y;
+}
+
+}  // namespace
+
+int launch_sppf(int dtype, const PoolArgs& a, hipStream_t s) {
+    switch (dtype) {
+        case F32: return launch_sppf_t<float>(a, s);
+        case F16: return launch_sppf_t<_Float16>(a, s);
+        case BF16: return launch_sppf_t<__bf16>(a, s);
+    }
+    return (int)hipErrorInvalidValue;
+}
+
+int launch_attention(int dtype, const AttnArgs& a, int B, hipStream_t s) {
+    switch (dtype) {
+        case F32: return launch_attention_t<float>(a, B, s);
+        case F16: return launch_attention_t<_Float16>(a, B, s);
+        case BF16: return launch_attention_t<__bf16>(a, B, s);
+    }
+    return (int)hipErrorInvalidValue;
+}
+
+int launch_decode(int dtype, const DecodeArgs& a, hipStream_t s) {
+    switch (dtype) {
+        case F32: return launch_decode_t<float>(a, s);
+        case F16: return launch_decode_t<_Float16>(a, s);
+        case BF16: return launch_decode_t<__bf16>(a, s);
+    }
+    return (int)hipErrorInvalidValue;
+}
+
+int launch_set_io(void** io, const void* x, void* y, hipStream_t s) {
+    hipLaunchKernelGGL(set_io, dim3(1), dim3(1), 0, s, io, x, y);
+    return (int)hipGetLastError();
+}
+
+}  // namespace yh

@@ -1,0 +1,73 @@
+"""Drop-in for the hot-path helpers of the reference's `utils/util.py`.
+
+  make_anchors          reference utils/util.py:85-96 (grid centres + stride per anchor)
+  wh2xy                 reference utils/util.py:76-82
+  non_max_suppression   reference utils/util.py:123-169, run on device by the gfx950
+                        kernels behind include/yolo_hip.h (yh_nms)
+  setup_seed            reference utils/util.py:12-20
+
+non_max_suppression semantics: candidate (anchor, class) pairs with score >
+threshold (compared in the tensor dtype), score-descending order with ties
+broken by the lower anchor*nc + class index (the reference's argsort is
+unstable, util.py:157), first 30000 kept, class-offset boxes (class * 7680),
+greedy IoU > threshold suppression (torchvision.ops.nms contract), first 300
+kept. Deliberate differences: no wall-clock cutoff (util.py:133-134,166-167
+silently truncates batches); box geometry is evaluated in fp32 for fp16/bf16
+inputs (in fp16 the reference's class offset 7680*c overflows for c >= 9).
+"""
+import random
+
+import numpy
+import torch
+
+__all__ = ["setup_seed", "wh2xy", "make_anchors", "non_max_suppression"]
+
+MAX_WH = 7680
+MAX_DET = 300
+MAX_NMS = 30000
+
+
+def setup_seed():
+    random.seed(0)
+    numpy.random.seed(0)
+    torch.manual_seed(0)
+    torch.backends.cudnn.benchmark = False
+    torch.backends.cudnn.deterministic = True
+
+
+def wh2xy(x):
+    """(cx, cy, w, h) -> (x1, y1, x2, y2) for an (n, 4+) tensor or array."""
+    y = x.clone() if isinstance(x, torch.Tensor) else numpy.copy(x)
+    half_w, half_h = x[:, 2] / 2, x[:, 3] / 2
+    y[:, 0] = x[:, 0] - half_w
+    y[:, 1] = x[:, 1] - half_h
+    y[:, 2] = x[:, 0] + half_w
+    y[:, 3] = x[:, 1] + half_h
+    return y
+
+
+def make_anchors(x, strides, offset=0.5):
+    """Per-level grid centres (x + offset, y + offset), row-major, and the level stride per anchor."""
+    assert x is not None
+    points, stride_col = [], []
+    dtype, device = x[0].dtype, x[0].device
+    for level, stride in enumerate(strides):
+        h, w = x[level].shape[-2:]
+        gx = torch.arange(end=w, device=device, dtype=dtype) + offset
+        gy = torch.arange(end=h, device=device, dtype=dtype) + offset
+        gy, gx = torch.meshgrid(gy, gx, indexing="ij")
+        points.append(torch.stack((gx, gy), -1).view(-1, 2))
+        stride_col.append(torch.full((h * w, 1), stride, dtype=dtype, device=device))
+    return torch.cat(points), torch.cat(stride_col)
+
+
+def non_max_suppression(outputs, confidence_threshold=0.001, iou_threshold=0.65):
+    """(B, 4 + nc, A) head outputs -> list of B tensors (k <= 300, 6) = x1, y1, x2, y2, score, class."""
+    if not outputs.is_cuda:
+        raise NotImplementedError("utils.util.non_max_suppression runs on the MI355X (cuda/HIP) device; "
+                                  "move the head outputs to cuda first")
+    from yolo_hip.engine import nms
+
+    dets, counts = nms(outputs, confidence_threshold, iou_threshold, MAX_DET, MAX_NMS, float(MAX_WH))
+    kept = counts.tolist()
+    return [dets[i, :k].to(outputs.dtype) for i, k in enumerate(kept)]
