@@ -1,0 +1,217 @@
+"""Headline benchmark: YOLOv11n eval forward + on-device NMS, 640x640, batch 32 per GPU.
+
+BASELINE.json metric: images/sec at 640x640 batch 32, v11_n, 1/2/4/8 MI355X.
+A step = one pass of the hot path over one batch resident in HBM: the HIP
+forward (yh_forward, replayed as a HIP graph), the on-device NMS (yh_nms) and,
+for N > 1, the RCCL gather of the fixed-size detection buffers to rank 0.
+Data-parallel: every rank processes its own batch of 32 (weak scaling).
+
+  python bench.py [--gpus N] [--steps K] [--warmup W]
+  python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 ... bench.py --gpus N
+
+Prints ONE JSON line on rank 0 (fields per the driver contract), including
+`roofline` (dominant kernel family: the dense 3x3 implicit-GEMM convs, timed
+with HIP events per launch on the forward's stream) and `cpu_baseline` (the CPU
+oracle, fp32 forward + NMS, on the host cores, N=1 only).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+for p in (ROOT, os.path.join(ROOT, "yolo-infer-pt_amd")):
+    if p not in sys.path:
+        sys.path.insert(0, p)
+
+HBM_PEAK_GBS = 8000.0       # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+MFMA_PEAK_TFLOPS = {"bf16": 2500.0, "fp16": 2500.0, "fp32": 157.3}  # dense, spec
+DTYPES = {"bf16": torch.bfloat16, "fp16": torch.float16, "fp32": torch.float32}
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def build_model(variant):
+    from nets import nn
+    from yolo_hip import synth
+    torch.manual_seed(0)
+    model = getattr(nn, f"yolo_v11_{variant}")(80)
+    model.load_state_dict(synth.synth_state_dict(model.state_dict(), seed=0))
+    return model.eval()
+
+
+def roofline(eng, args, batch, prof_steps, x, y):
+    """Per-launch HIP-event timing of every op over `prof_steps` forwards (same stream)."""
+    eng.profile(True)
+    eng.profile_reset()
+    for _ in range(prof_steps):
+        eng.forward(x, out=y)
+    eng.profile(False)
+    ops = eng.ops(batch, args.size, args.size)
+    by_cls = {}
+    for o in ops:
+        c = by_cls.setdefault(o["cls"], dict(ms=0.0, bytes=0.0, flops=0.0, launches=0, attain_ms=0.0))
+        avg_ms = o["ms"] / max(1, o["calls"])
+        c["ms"] += avg_ms
+        c["bytes"] += o["bytes"]
+        c["flops"] += o["flops"]
+        c["launches"] += 1
+        peak_tf = MFMA_PEAK_TFLOPS[args.dtype] if o["cls"] in ("conv3x3", "conv1x1") else 157.3
+        c["attain_ms"] += max(o["bytes"] / (HBM_PEAK_GBS * 1e9), o["flops"] / (peak_tf * 1e12)) * 1e3
+    total = sum(c["ms"] for c in by_cls.values())
+    for k, c in sorted(by_cls.items(), key=lambda kv: -kv[1]["ms"]):
+        log(f"  {k:10s} {c['launches']:3d} launches  {c['ms'] * 1e3:8.1f} us/fwd ({100 * c['ms'] / total:4.1f}%)  "
+            f"{c['bytes'] / c['ms'] / 1e6:7.0f} GB/s  {c['flops'] / c['ms'] / 1e9:7.1f} TFLOP/s  "
+            f"attainable {100 * c['attain_ms'] / c['ms']:4.1f}%")
+    dom = by_cls["conv3x3"]
+    achieved = dom["bytes"] / dom["ms"] / 1e6  # GB/s
+    return dict(bound="hbm", achieved=round(achieved, 1), peak=HBM_PEAK_GBS, unit="GB/s",
+                frac=round(achieved / HBM_PEAK_GBS, 4), traffic=None,
+                kernel="conv_gemm, dense 3x3 convs (implicit-GEMM MFMA)",
+                launches_per_step=dom["launches"],
+                avg_launch_us=round(dom["ms"] * 1e3 / dom["launches"], 2),
+                algorithmic_bytes_per_launch=round(dom["bytes"] / dom["launches"]),
+                attainable_frac=round(dom["attain_ms"] / dom["ms"], 4),
+                forward_kernel_ms=round(total, 4))
+
+
+def cpu_baseline(args, min_seconds=10.0, max_seconds=30.0):
+    """The CPU oracle (fp32 functional forward + numpy NMS) on a bounded sample of the workload."""
+    from oracle import nms as onms
+    from oracle.forward import Oracle
+    from yolo_hip import synth
+    from yolo_hip.variants import VARIANTS
+
+    threads = min(16, os.cpu_count() or 1)
+    torch.set_num_threads(threads)
+    model = build_model(args.variant)
+    v = VARIANTS[args.variant]
+    orc = Oracle(model.state_dict(), v.width, v.depth, v.csp, 80, dtype=torch.float32)
+    per = 4
+    x = synth.synth_scenes(per, args.size, args.size, seed=1000)
+    orc(x[:1])  # warm-up
+    n, t0 = 0, time.perf_counter()
+    while True:
+        y = orc(x)
+        onms.non_max_suppression(y.numpy())
+        n += per
+        dt = time.perf_counter() - t0
+        if dt >= min_seconds or dt >= max_seconds:
+            break
+    return dict(value=round(n / dt, 3), unit="images/s", cores=threads, kind="port",
+                sample=f"{n} images ({n // per} batches of {per}) of the same workload "
+                       f"(v11_{args.variant} {args.size}x{args.size}, fp32 oracle forward + numpy NMS), {dt:.1f} s")
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--variant", default="n")
+    ap.add_argument("--size", type=int, default=640)
+    ap.add_argument("--batch", type=int, default=32, help="images per GPU per step")
+    ap.add_argument("--dtype", default="bf16", choices=sorted(DTYPES))
+    ap.add_argument("--profile-steps", type=int, default=None)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-roofline", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = world > 1
+    if dist:
+        torch.cuda.set_device(local)
+        torch.distributed.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+    dtype = DTYPES[args.dtype]
+
+    from yolo_hip import synth
+    from yolo_hip.engine import Engine, nms
+
+    model = build_model(args.variant)
+    eng = Engine(*model._yh_arch, dev, dtype)
+    eng.load_module(model)
+    B, S = args.batch, args.size
+    eng.reserve(B, S, S)
+    # synthetic scenes, one distinct batch per rank, resident in HBM before timing
+    x = synth.synth_scenes(B, S, S, seed=100 + rank).to(dev, dtype)
+    A = eng.num_anchors(S, S)
+    y = torch.empty((B, 84, A), dtype=dtype, device=dev)
+    gathered = [torch.empty((B, 300 * 6 + 1), device=dev) for _ in range(world)] if (dist and rank == 0) else None
+
+    def step():
+        eng.forward(x, out=y)
+        dets, counts = nms(y)
+        if dist:
+            packed = torch.cat((dets.view(B, -1), counts.view(B, 1).float()), 1)
+            torch.distributed.gather(packed, gathered, dst=0)
+        return counts
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if dist:
+        torch.distributed.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        counts = step()
+    torch.cuda.synchronize()
+    if dist:
+        torch.distributed.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    if dist:
+        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+        elapsed = t.item()
+    kept = counts.cpu().tolist()
+
+    roof = None
+    if not args.no_roofline:
+        if rank == 0:
+            log(f"per-class kernel time (HIP events, {args.profile_steps or args.steps} forwards, batch {B}):")
+        roof = roofline(eng, args, B, args.profile_steps or args.steps, x, y)
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(args)
+
+    if rank == 0:
+        imgs = B * world * args.steps
+        value = imgs / elapsed
+        rec = {
+            "metric": "images/sec at 640x640 batch32, v11_n (forward + on-device NMS)",
+            "value": round(value, 2),
+            "unit": "images/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": args.dtype,
+            "data": "synthetic (seeded scenes; calibrated synthetic weights)",
+            "config": {"workload": f"yolo_v11_{args.variant} eval forward + NMS, {S}x{S}, {B} images per GPU per step",
+                       "per_gpu_batch": B, "global_batch": B * world, "image_size": S,
+                       "parallelism": f"dp{world}", "nms": "on-device, conf 0.001, iou 0.65, max_det 300"},
+            "roofline": roof,
+            "cpu_baseline": cpu,
+            "kept_last_step": kept[:4],
+        }
+        print(json.dumps(rec), flush=True)
+    if dist:
+        torch.distributed.barrier()
+        torch.distributed.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -2,7 +2,8 @@
 
 The shared library is built in-tree by `make` (or __graft_entry__.build()) next
 to this file. Loading it does not touch the GPU; every compute entry point
-needs a HIP device. There is deliberately no fallback: if the library cannot
+needs a HIP device. torch is imported before the library is opened so both use
+PyTorch's HIP runtime. There is deliberately no fallback: if the library cannot
 be loaded, GPU inference raises.
 """
 import ctypes
@@ -57,6 +58,11 @@ def lib():
     """Load (once) and return the ctypes library; raises if it is missing."""
     global _lib
     if _lib is None:
+        # PyTorch-ROCm ships its own libamdhip64.so.7. Importing torch first makes the
+        # dynamic loader resolve our DT_NEEDED libamdhip64.so.7 to that same runtime,
+        # so the library and torch share one HIP runtime (streams, graphs, memory).
+        # Loading ours first would bring in /opt/rocm's copy next to torch's.
+        import torch  # noqa: F401
         if not os.path.exists(LIB_PATH):
             raise RuntimeError(
                 f"yolo_hip: {LIB_PATH} not found; build it with `make` (or __graft_entry__.build())")
