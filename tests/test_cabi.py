@@ -47,7 +47,7 @@ def test_abi_version_and_error_path():
 def test_nms_workspace_bytes():
     from yolo_hip import _lib
     lib = _lib.lib()
-    assert lib.yh_nms_workspace_bytes(2, 80, 8400) == 2 * 8400 * 80 * 8 + 2 * 4 + 256
+    assert lib.yh_nms_workspace_bytes(2, 80, 8400) == 2 * 8400 * 80 * 8 + 2 * 4 + 2 * 2048 * 4 + 512
     assert lib.yh_nms_workspace_bytes(0, 80, 8400) == 0
 
 

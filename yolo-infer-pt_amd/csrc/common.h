@@ -30,6 +30,7 @@ struct ConvArgs {
     int Cout;            // physical output channels written (multiple of 8)
     int act;
     int gm, gn;          // tile grid
+    const void* zero;    // >= 16 zero bytes in device memory (source of padded taps)
 };
 
 // First layer: 3-channel NCHW input (the caller's tensor), 3x3 stride-2 conv.
@@ -85,6 +86,8 @@ struct NmsArgs {
     int max_det, max_nms;
     unsigned long long* keys;  // [B][A*nc] candidate keys
     int* counts;               // [B] candidate counts (zeroed by the launcher)
+    unsigned* hist;            // [B][2048] coarse score-bin histogram (zeroed by the launcher)
+    int bin_base;              // (fp32 bits >> 16) of the lowest bin
     float* dets; int* ndet;
 };
 

@@ -11,12 +11,19 @@
 // Reference semantics: Conv.fuse_forward (nets/nn.py:38-39) = act(conv'(x)) with
 // the BN folded into conv' (fuse_conv, nets/nn.py:8-25); Residual (nn.py:48-49)
 // = x + act(conv'(...)) -> residual added after the activation.
+#include <cstdlib>
+
 #include "common.h"
 #include "dtypes.h"
 
 namespace yh {
 
 namespace {
+
+int env_int(const char* name, int dflt) {
+    const char* e = getenv(name);
+    return e ? atoi(e) : dflt;
+}
 
 constexpr int BK = 32;        // reduction depth per stage (one 16x16x32 MFMA)
 constexpr int LDK = BK + 8;   // padded LDS row (elements) to spread banks
@@ -206,6 +213,528 @@ __global__ __launch_bounds__(NT_) void conv_gemm(const ConvArgs p) {
     }
 }
 
+// ---------------------------------------------------------------------------
+// conv_gemm2: the 16-bit (bf16 / fp16) implicit GEMM.
+//   * activation and weight tiles go HBM -> LDS by LDS-DMA (global_load_lds,
+//     16 B per lane, no VGPR staging), two 64-deep K stages in flight: the DMA
+//     of stage k+1 overlaps the MFMAs of stage k;
+//   * LDS rows are 128 B (64 k of one pixel / one cout); the eight 16-B slots of
+//     row r are XOR-swizzled by (r & 7) through the per-lane SOURCE address, so
+//     the DMA writes linearly and the 16-lane ds_read_b128 fragment reads hit 64
+//     distinct banks;
+//   * padding taps / channels read a 16-B zero page instead of branching.
+constexpr int BK2 = 64;
+
+// 16-byte LDS-DMA: lane i writes lds_base + 16*i (lds_base wave-uniform).
+// Device-only builtin: kept out of the host pass so the kernel's host handle is emitted.
+__device__ __forceinline__ void glds16(const void* src, char* lds_base) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    typedef __attribute__((address_space(3))) void* lds_void_ptr;
+    __builtin_amdgcn_global_load_lds(src, (lds_void_ptr)lds_base, 16, 0, 0);
+#else
+    (void)src; (void)lds_base;
+#endif
+}
+
+// The same DMA hidden from hipcc's waitcnt pass (inline asm): the compiler then
+// cannot insert the conservative vmcnt(0) in front of every ds_read of the ring
+// (it cannot prove the reads miss the in-flight DMA slots). Ordering comes only
+// from the kernel's own counted s_waitcnt vmcnt + barrier. M0 is saved/restored
+// inside the statement (MI355X guide, section 5.7).
+__device__ __forceinline__ void glds16_asm(const void* src, const char* lds_base) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    typedef __attribute__((address_space(3))) const char* lds_cptr;
+    const unsigned lds_addr = __builtin_amdgcn_readfirstlane((unsigned)(size_t)(lds_cptr)lds_base);
+    unsigned keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep) : "v"(src), "s"(lds_addr) : "memory");
+#else
+    (void)src; (void)lds_base;
+#endif
+}
+
+template <int BM, int BN>
+struct Smem2 {
+    static constexpr int A_BYTES = BM * 128;
+    static constexpr int B_BYTES = BN * 128;
+    static constexpr int STAGE = A_BYTES + B_BYTES;
+    static constexpr int MAIN = 2 * STAGE;
+    static constexpr int EPI = BM * (BN + 8) * 2;
+    static constexpr int REGION = MAIN > EPI ? MAIN : EPI;
+};
+
+template <typename T, int BM, int BN>
+__global__ __launch_bounds__(NT_) void conv_gemm2(const ConvArgs p) {
+    static_assert(sizeof(T) == 2, "16-bit path");
+    static_assert(BM % 64 == 0 && BN % 16 == 0, "tile");
+    constexpr int MT = BM / 64;
+    constexpr int NTL = BN / 16;
+    constexpr int AI = BM / 32;   // A wave-instructions (8 rows x 128 B) per wave per stage
+    using SM = Smem2<BM, BN>;
+
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    int* ktab = reinterpret_cast<int*>(smem + SM::REGION);
+
+    const int tid = threadIdx.x;
+    const int lane = tid & 63, wave = tid >> 6;
+    const int lid = xcd_remap(blockIdx.x, p.gm * p.gn);
+    const int mt = lid / p.gn, nt = lid - mt * p.gn;
+    const int m0 = mt * BM, n0 = nt * BN;
+    for (int i = tid; i < p.Kp / 8; i += NT_) ktab[i] = p.ktab[i];
+
+    const int lrow = lane >> 3;                 // row within a DMA instruction
+    const int cidx = (lane & 7) ^ lrow;         // logical 16-B chunk this lane fetches
+    const int HoWo = p.Ho * p.Wo;
+    int rn[AI], rhb[AI], rwb[AI];
+#pragma unroll
+    for (int i = 0; i < AI; ++i) {
+        const int m = m0 + (wave + 4 * i) * 8 + lrow;
+        if (m < p.M) {
+            const int n = m / HoWo, r = m - n * HoWo;
+            const int ho = r / p.Wo, wo = r - ho * p.Wo;
+            rn[i] = n; rhb[i] = ho * p.stride - p.pad; rwb[i] = wo * p.stride - p.pad;
+        } else {
+            rn[i] = -1; rhb[i] = 0; rwb[i] = 0;
+        }
+    }
+    const T* in0 = reinterpret_cast<const T*>(p.in0);
+    const T* in1 = reinterpret_cast<const T*>(p.in1);
+    const T* wg = reinterpret_cast<const T*>(p.w);
+    const long long bs0 = (long long)p.h0 * p.w0 * p.ldc0;
+    const long long bs1 = (long long)p.h1 * p.w1 * p.ldc1;
+    __syncthreads();  // ktab
+
+    auto issue = [&](int kt, int buf) {
+        char* a = smem + buf * SM::STAGE;
+        char* b = a + SM::A_BYTES;
+        const int e = ktab[kt * 8 + cidx];
+        const int kh = e >> 24, kw = (e >> 16) & 0xff, ci = e & 0xffff;
+#pragma unroll
+        for (int i = 0; i < AI; ++i) {
+            const int hi = rhb[i] + kh, wi = rwb[i] + kw;
+            const void* src = p.zero;
+            if (ci != 0xffff && rn[i] >= 0 && hi >= 0 && hi < p.Hi && wi >= 0 && wi < p.Wi) {
+                if (ci < p.c0)
+                    src = in0 + rn[i] * bs0 + ((long long)(hi >> p.up0) * p.w0 + (wi >> p.up0)) * p.ldc0 + ci;
+                else
+                    src = in1 + rn[i] * bs1 + ((long long)(hi >> p.up1) * p.w1 + (wi >> p.up1)) * p.ldc1 + (ci - p.c0);
+            }
+            glds16(src, a + (wave + 4 * i) * 1024);
+        }
+        for (int ii = wave; ii < BN / 8; ii += 4) {
+            const T* src = wg + (long long)(n0 + ii * 8 + lrow) * p.Kp + kt * BK2 + cidx * 8;
+            glds16(src, b + ii * 1024);
+        }
+    };
+
+    f32x4 acc[NTL][MT];
+#pragma unroll
+    for (int i = 0; i < NTL; ++i)
+#pragma unroll
+        for (int j = 0; j < MT; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    const int nkt = p.Kp / BK2;
+    const int fr = lane & 15, fq = lane >> 4;
+    issue(0, 0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    for (int kt = 0; kt < nkt; ++kt) {
+        const int cur = kt & 1;
+        if (kt + 1 < nkt) issue(kt + 1, cur ^ 1);
+        const char* a = smem + cur * SM::STAGE;
+        const char* b = a + SM::A_BYTES;
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk) {
+            const int chunk = kk * 4 + fq;
+            uint4 wf[NTL];
+#pragma unroll
+            for (int i = 0; i < NTL; ++i) {
+                const int row = i * 16 + fr;
+                wf[i] = *reinterpret_cast<const uint4*>(b + row * 128 + ((chunk ^ (row & 7)) << 4));
+            }
+#pragma unroll
+            for (int j = 0; j < MT; ++j) {
+                const int row = wave * (BM / 4) + j * 16 + fr;
+                const uint4 xa = *reinterpret_cast<const uint4*>(a + row * 128 + ((chunk ^ (row & 7)) << 4));
+#pragma unroll
+                for (int i = 0; i < NTL; ++i) Mma<T>::step(acc[i][j], &wf[i], &xa);
+            }
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+    }
+
+    constexpr int LDE = BN + 8;
+    T* Cs = reinterpret_cast<T*>(smem);
+#pragma unroll
+    for (int i = 0; i < NTL; ++i) {
+        const int co = i * 16 + fq * 4;
+        float bv[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) bv[r] = p.bias[n0 + co + r];
+#pragma unroll
+        for (int j = 0; j < MT; ++j) {
+            const int px = wave * (BM / 4) + j * 16 + fr;
+            T* dst = Cs + px * LDE + co;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                float v = acc[i][j][r] + bv[r];
+                if (p.act == ACT_SILU) v = silu<T>(v);
+                dst[r] = fromf<T>(v);
+            }
+        }
+    }
+    __syncthreads();
+    const T* res = reinterpret_cast<const T*>(p.res);
+    T* out = reinterpret_cast<T*>(p.out);
+    constexpr int CPP = BN / 8;
+    for (int c = tid; c < BM * CPP; c += NT_) {
+        const int px = c / CPP, cc = c - px * CPP;
+        const int m = m0 + px, co = n0 + cc * 8;
+        if (m >= p.M || co >= p.Cout) continue;
+        Chunk<T> v = ld_chunk(Cs + px * LDE + cc * 8);
+        if (res) {
+            float f[8], g[8];
+            chunk_to_f(v, f);
+            chunk_to_f(ld_chunk(res + (long long)m * p.ldr + co), g);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) f[e] += g[e];
+            v = f_to_chunk<T>(f);
+        }
+        st_chunk(out + (long long)m * p.ldo + co, v);
+    }
+}
+
+// ---------------------------------------------------------------------------
+// conv_stream: persistent, software-pipelined version of conv_gemm2 for the
+// 16-bit types. Each workgroup walks a contiguous run of (M-tile, N-tile) pairs
+// of its XCD and streams their 64-deep K stages through an NS-slot LDS ring by
+// LDS-DMA, keeping NS-1 stages in flight across tile boundaries (the epilogue
+// of one tile overlaps the DMA of the next tiles). Every wave issues exactly
+// LPS DMA instructions per stage (short B tiles and non-final stages pad with
+// zero-page DMAs into a scratch KiB), so one counted `s_waitcnt vmcnt` retires a
+// stage; barriers are raw s_barrier so nothing drains the DMA queue. The
+// residual (nets/nn.py:49,135-136) is fetched by inline-asm loads issued one
+// stage ahead of its use and waited with a counted vmcnt.
+template <int BM, int BN, int NS, bool RES>
+struct SmemS {
+    static constexpr int A_BYTES = BM * 128;
+    static constexpr int B_BYTES = BN * 128;
+    static constexpr int STAGE = A_BYTES + B_BYTES;
+    static constexpr int RING = NS * STAGE;
+    static constexpr int DUMMY = RING;                  // 1 KiB sink for padding DMAs
+    static constexpr int EPI = DUMMY + 1024;            // [BM][BN+8] output tile
+    static constexpr int EPI_BYTES = BM * (BN + 8) * 2;
+    static constexpr int TAIL = EPI + EPI_BYTES;        // ktab, bias follow
+};
+
+__device__ __forceinline__ void vm_wait(int n) {
+    // counted wait; n is wave-uniform and small
+    switch (n) {
+        case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+        case 1: asm volatile("s_waitcnt vmcnt(1)" ::: "memory"); break;
+        case 2: asm volatile("s_waitcnt vmcnt(2)" ::: "memory"); break;
+        case 3: asm volatile("s_waitcnt vmcnt(3)" ::: "memory"); break;
+        case 4: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
+        case 5: asm volatile("s_waitcnt vmcnt(5)" ::: "memory"); break;
+        case 6: asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); break;
+        case 7: asm volatile("s_waitcnt vmcnt(7)" ::: "memory"); break;
+        case 8: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
+        case 9: asm volatile("s_waitcnt vmcnt(9)" ::: "memory"); break;
+        case 10: asm volatile("s_waitcnt vmcnt(10)" ::: "memory"); break;
+        case 11: asm volatile("s_waitcnt vmcnt(11)" ::: "memory"); break;
+        case 12: asm volatile("s_waitcnt vmcnt(12)" ::: "memory"); break;
+        case 13: asm volatile("s_waitcnt vmcnt(13)" ::: "memory"); break;
+        case 14: asm volatile("s_waitcnt vmcnt(14)" ::: "memory"); break;
+        case 15: asm volatile("s_waitcnt vmcnt(15)" ::: "memory"); break;
+        case 16: asm volatile("s_waitcnt vmcnt(16)" ::: "memory"); break;
+        case 18: asm volatile("s_waitcnt vmcnt(18)" ::: "memory"); break;
+        case 20: asm volatile("s_waitcnt vmcnt(20)" ::: "memory"); break;
+        case 24: asm volatile("s_waitcnt vmcnt(24)" ::: "memory"); break;
+        case 30: asm volatile("s_waitcnt vmcnt(30)" ::: "memory"); break;
+        case 32: asm volatile("s_waitcnt vmcnt(32)" ::: "memory"); break;
+        default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+    }
+}
+
+__device__ __forceinline__ void lds_barrier() {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+}
+
+template <typename T, int BM, int BN, int NS, bool RES>
+__global__ __launch_bounds__(NT_) void conv_stream(const ConvArgs p) {
+    static_assert(sizeof(T) == 2, "16-bit path");
+    constexpr int MT = BM / 64;
+    constexpr int NTL = BN / 16;
+    constexpr int AI = BM / 32;                        // A DMA instructions per wave per stage
+    constexpr int BI = BN / 32 > 0 ? BN / 32 : 1;      // B DMA instructions per wave per stage
+    constexpr int CPP = BN / 8;                        // 16-B chunks per output pixel row
+    constexpr int RPW = (BM * CPP) / NT_ > 0 ? (BM * CPP) / NT_ : 1;  // residual chunks per thread
+    constexpr int LPS = AI + BI;
+    using SM = SmemS<BM, BN, NS, RES>;
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    int* ktab = reinterpret_cast<int*>(smem + SM::TAIL);
+    float* bias_s = reinterpret_cast<float*>(smem + SM::TAIL + p.Kp / 8 * 4);
+
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int ntiles = p.gm * p.gn;
+    // contiguous tile range per XCD (blocks b and b+8 share an XCD), round-robin inside it
+    const int nblk = gridDim.x, xcd = blockIdx.x & 7, q = blockIdx.x >> 3, per_xcd = nblk >> 3;
+    const int t_lo = (int)(((long long)ntiles * xcd) / 8), t_hi = (int)(((long long)ntiles * (xcd + 1)) / 8);
+    const int my_tiles = t_hi - t_lo > q ? (t_hi - t_lo - q + per_xcd - 1) / per_xcd : 0;
+    const int nkt = p.Kp / BK2;
+    const int total = my_tiles * nkt;
+
+    for (int i = tid; i < p.Kp / 8; i += NT_) ktab[i] = p.ktab[i];
+    for (int i = tid; i < p.gn * BN; i += NT_) bias_s[i] = p.bias[i];
+    __syncthreads();   // no DMA in flight yet: the plain barrier is free here
+    if (total == 0) return;
+
+    const int lrow = lane >> 3, cidx = (lane & 7) ^ lrow;
+    const int HoWo = p.Ho * p.Wo;
+    const T* in0 = reinterpret_cast<const T*>(p.in0);
+    const T* in1 = reinterpret_cast<const T*>(p.in1);
+    const T* wg = reinterpret_cast<const T*>(p.w);
+    const long long bs0 = (long long)p.h0 * p.w0 * p.ldc0;
+    const long long bs1 = (long long)p.h1 * p.w1 * p.ldc1;
+
+    // issue-side state
+    int iss = 0, iss_tile = -1, iss_m0 = 0, iss_n0 = 0;
+    int rn[AI], rhb[AI], rwb[AI];
+    auto tile_of = [&](int j, int& m0, int& n0) {
+        const int t = t_lo + q + j * per_xcd;
+        const int mt = t / p.gn, nt = t - mt * p.gn;
+        m0 = mt * BM; n0 = nt * BN;
+    };
+    auto issue = [&]() {
+        char* slot = smem + (iss % NS) * SM::STAGE;
+        if (iss < total) {
+            const int j = iss / nkt, kt = iss - j * nkt;
+            if (j != iss_tile) {
+                iss_tile = j;
+                tile_of(j, iss_m0, iss_n0);
+#pragma unroll
+                for (int i = 0; i < AI; ++i) {
+                    const int m = iss_m0 + (wave + 4 * i) * 8 + lrow;
+                    if (m < p.M) {
+                        const int n = m / HoWo, r = m - n * HoWo;
+                        const int ho = r / p.Wo, wo = r - ho * p.Wo;
+                        rn[i] = n; rhb[i] = ho * p.stride - p.pad; rwb[i] = wo * p.stride - p.pad;
+                    } else {
+                        rn[i] = -1; rhb[i] = 0; rwb[i] = 0;
+                    }
+                }
+            }
+            const int e = ktab[kt * 8 + cidx];
+            const int kh = e >> 24, kw = (e >> 16) & 0xff, ci = e & 0xffff;
+#pragma unroll
+            for (int i = 0; i < AI; ++i) {
+                const int hi = rhb[i] + kh, wi = rwb[i] + kw;
+                const void* src = p.zero;
+                if (ci != 0xffff && rn[i] >= 0 && hi >= 0 && hi < p.Hi && wi >= 0 && wi < p.Wi) {
+                    if (ci < p.c0)
+                        src = in0 + rn[i] * bs0 + ((long long)(hi >> p.up0) * p.w0 + (wi >> p.up0)) * p.ldc0 + ci;
+                    else
+                        src = in1 + rn[i] * bs1 + ((long long)(hi >> p.up1) * p.w1 + (wi >> p.up1)) * p.ldc1 + (ci - p.c0);
+                }
+                glds16_asm(src, slot + (wave + 4 * i) * 1024);
+            }
+#pragma unroll
+            for (int i = 0; i < BI; ++i) {
+                const int ii = wave + 4 * i;
+                if (ii < BN / 8) {
+                    const T* src = wg + (long long)(iss_n0 + ii * 8 + lrow) * p.Kp + kt * BK2 + cidx * 8;
+                    glds16_asm(src, slot + SM::A_BYTES + ii * 1024);
+                } else {
+                    glds16_asm(p.zero, smem + SM::DUMMY);
+                }
+            }
+        } else {
+            // pipeline tail: keep the per-stage count uniform with zero-page DMAs
+#pragma unroll
+            for (int i = 0; i < LPS; ++i) glds16_asm(p.zero, smem + SM::DUMMY);
+        }
+        ++iss;
+    };
+
+    f32x4 acc[NTL][MT];
+#pragma unroll
+    for (int i = 0; i < NTL; ++i)
+#pragma unroll
+        for (int j = 0; j < MT; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+#pragma unroll
+    for (int sidx = 0; sidx < NS - 1; ++sidx) issue();
+
+    const int fr = lane & 15, fq = lane >> 4;
+    const T* res = reinterpret_cast<const T*>(p.res);
+    T* out = reinterpret_cast<T*>(p.out);
+    T* Cs = reinterpret_cast<T*>(smem + SM::EPI);
+    constexpr int LDE = BN + 8;
+    for (int g = 0; g < total; ++g) {
+        vm_wait(LPS * (NS - 2));   // this wave's DMAs of stage g have landed
+        lds_barrier();             // ... and everyone's; everyone is done with stage g-1
+        const int j = g / nkt, kt = g - j * nkt;
+        const bool last = kt == nkt - 1;
+        int m0, n0;
+        tile_of(j, m0, n0);
+        static_assert(!RES || RPW <= 4, "residual chunks per thread");
+        typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+        u32x4 rv0 = {0u, 0u, 0u, 0u}, rv1 = rv0, rv2 = rv0, rv3 = rv0;
+        if constexpr (RES) {
+            if (last) {  // residual of this tile, issued before the next stage's DMA
+                auto rsrc = [&](int r) {
+                    const int c = tid + r * NT_;
+                    const int px = c / CPP, cc = c - px * CPP;
+                    const int m = min(m0 + px, p.M - 1), co = min(n0 + cc * 8, p.Cout - 8);
+                    return res + (long long)m * p.ldr + co;
+                };
+                asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(rv0) : "v"(rsrc(0)) : "memory");
+                if constexpr (RPW > 1) asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(rv1) : "v"(rsrc(1)) : "memory");
+                if constexpr (RPW > 2) asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(rv2) : "v"(rsrc(2)) : "memory");
+                if constexpr (RPW > 3) asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(rv3) : "v"(rsrc(3)) : "memory");
+            }
+        }
+        issue();   // stage g + NS - 1 into the slot stage g-1 used
+        const char* a = smem + (g % NS) * SM::STAGE;
+        const char* b = a + SM::A_BYTES;
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk) {
+            const int chunk = kk * 4 + fq;
+            uint4 wf[NTL];
+#pragma unroll
+            for (int i = 0; i < NTL; ++i) {
+                const int row = i * 16 + fr;
+                wf[i] = *reinterpret_cast<const uint4*>(b + row * 128 + ((chunk ^ (row & 7)) << 4));
+            }
+#pragma unroll
+            for (int jj = 0; jj < MT; ++jj) {
+                const int row = wave * (BM / 4) + jj * 16 + fr;
+                const uint4 xa = *reinterpret_cast<const uint4*>(a + row * 128 + ((chunk ^ (row & 7)) << 4));
+#pragma unroll
+                for (int i = 0; i < NTL; ++i) Mma<T>::step(acc[i][jj], &wf[i], &xa);
+            }
+        }
+        if (last) {
+#pragma unroll
+            for (int i = 0; i < NTL; ++i) {
+                const int co = i * 16 + fq * 4;
+#pragma unroll
+                for (int jj = 0; jj < MT; ++jj) {
+                    const int px = wave * (BM / 4) + jj * 16 + fr;
+                    T* dst = Cs + px * LDE + co;
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        float v = acc[i][jj][r] + bias_s[n0 + co + r];
+                        if (p.act == ACT_SILU) v = silu<T>(v);
+                        dst[r] = fromf<T>(v);
+                    }
+                    acc[i][jj] = f32x4{0.f, 0.f, 0.f, 0.f};
+                }
+            }
+            lds_barrier();
+            if constexpr (RES) {
+                // the residual loads are older than the LPS DMAs just issued: vmcnt(LPS)
+                static_assert(LPS >= 3 && LPS <= 12, "residual wait count");
+#define YH_RWAIT(N) asm volatile("s_waitcnt vmcnt(" #N ")" : "+v"(rv0), "+v"(rv1), "+v"(rv2), "+v"(rv3) :: "memory")
+                if constexpr (LPS == 3) YH_RWAIT(3);
+                else if constexpr (LPS == 4) YH_RWAIT(4);
+                else if constexpr (LPS == 5) YH_RWAIT(5);
+                else if constexpr (LPS == 6) YH_RWAIT(6);
+                else if constexpr (LPS == 8) YH_RWAIT(8);
+                else if constexpr (LPS == 9) YH_RWAIT(9);
+                else if constexpr (LPS == 10) YH_RWAIT(10);
+                else YH_RWAIT(12);
+#undef YH_RWAIT
+            }
+#pragma unroll
+            for (int r = 0; r < RPW; ++r) {
+                const int c = tid + r * NT_;
+                if (c >= BM * CPP) break;
+                const int px = c / CPP, cc = c - px * CPP;
+                const int m = m0 + px, co = n0 + cc * 8;
+                Chunk<T> v = ld_chunk(Cs + px * LDE + cc * 8);
+                if constexpr (RES) {
+                    float f[8], gg[8];
+                    Chunk<T> rc;
+                    rc.v[0] = __builtin_bit_cast(uint4, r == 0 ? rv0 : r == 1 ? rv1 : r == 2 ? rv2 : rv3);
+                    chunk_to_f(v, f);
+                    chunk_to_f(rc, gg);
+#pragma unroll
+                    for (int e = 0; e < 8; ++e) f[e] += gg[e];
+                    v = f_to_chunk<T>(f);
+                }
+                if (m < p.M && co < p.Cout) st_chunk(out + (long long)m * p.ldo + co, v);
+            }
+        }
+    }
+    vm_wait(0);
+}
+
+template <typename T, int BM, int BN, int NS>
+int launch_stream_t(const ConvArgs& a, hipStream_t s, int blocks_per_cu) {
+    constexpr bool RES_OK = (BM * (BN / 8)) / NT_ <= 4;
+    const int lds_res = SmemS<BM, BN, NS, true>::TAIL + a.Kp / 8 * 4 + a.gn * BN * 4;
+    static bool attr[2] = {false, false};
+    const bool res = a.res != nullptr;
+    if (res && !RES_OK) return (int)hipErrorInvalidValue;
+    const int ntiles = a.gm * a.gn;
+    int grid = 256 * blocks_per_cu;
+    if (grid > ntiles) grid = ((ntiles + 7) / 8) * 8;
+    if constexpr (RES_OK) {
+        if (res) {
+            if (!attr[1]) {
+                (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_stream<T, BM, BN, NS, true>),
+                                          hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+                attr[1] = true;
+            }
+            hipLaunchKernelGGL((conv_stream<T, BM, BN, NS, true>), dim3(grid), dim3(NT_), lds_res, s, a);
+            return (int)hipGetLastError();
+        }
+    }
+    if (!attr[0]) {
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_stream<T, BM, BN, NS, false>),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        attr[0] = true;
+    }
+    hipLaunchKernelGGL((conv_stream<T, BM, BN, NS, false>), dim3(grid), dim3(NT_), lds_res, s, a);
+    return (int)hipGetLastError();
+}
+
+template <typename T, int BM, int BN>
+int launch_conv2_t(const ConvArgs& a, hipStream_t s) {
+    using SM = Smem2<BM, BN>;
+    const int lds = SM::REGION + (a.Kp / 8) * 4;
+    static bool attr_set = false;
+    if (!attr_set) {
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_gemm2<T, BM, BN>),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        attr_set = true;
+    }
+    hipLaunchKernelGGL((conv_gemm2<T, BM, BN>), dim3(a.gm * a.gn), dim3(NT_), lds, s, a);
+    return (int)hipGetLastError();
+}
+
+template <typename T>
+int launch_conv2_bm(int BM, int BN, const ConvArgs& a, hipStream_t s) {
+#define YH_BN2(bm)                                                       \
+    switch (BN) {                                                        \
+        case 16: return launch_conv2_t<T, bm, 16>(a, s);                 \
+        case 32: return launch_conv2_t<T, bm, 32>(a, s);                 \
+        case 64: return launch_conv2_t<T, bm, 64>(a, s);                 \
+        case 128: return launch_conv2_t<T, bm, 128>(a, s);               \
+        default: return (int)hipErrorInvalidValue;                       \
+    }
+    switch (BM) {
+        case 64: YH_BN2(64)
+        case 128: YH_BN2(128)
+        case 256: YH_BN2(256)
+        default: return (int)hipErrorInvalidValue;
+    }
+#undef YH_BN2
+}
+
 template <typename T, int BM, int BN>
 int launch_conv_t(const ConvArgs& a, hipStream_t s) {
     using SM = ConvSmem<T, BM, BN>;
@@ -239,67 +768,182 @@ int launch_conv_bm(int BM, int BN, const ConvArgs& a, hipStream_t s) {
 #undef YH_BN
 }
 
-template <typename T, int CPT>
-__global__ __launch_bounds__(256) void conv_first(const FirstConvArgs p) {
-    // Stem: Conv(3 -> Cout, k3, s2, p1) + act (nets/nn.py:161). One thread = one
-    // output pixel x CPT couts; the 27 taps are gathered once into registers and
-    // the weights ([27][Cout], packed on the host) are wave-uniform scalar loads.
-    const float* ws = p.w;
-    const float* bs = p.bias;
-    const int m = blockIdx.x * blockDim.x + threadIdx.x;
-    const int co0 = blockIdx.y * CPT;
-    if (m >= p.M) return;
-    const int HoWo = p.Ho * p.Wo;
-    const int n = m / HoWo, r = m - n * HoWo;
-    const int ho = r / p.Wo, wo = r - ho * p.Wo;
+// Stem: Conv(3 -> Cout, k3, s2, p1) + act (nets/nn.py:161) straight from the
+// caller's NCHW tensor. A block = STEM_TW consecutive output pixels of one output
+// row: the 3 channels x 3 input rows x (2*STEM_TW+1) columns it needs are
+// contiguous row segments in NCHW, staged into LDS with aligned 16-B loads
+// (one HBM read of the input, ~1.5x with the row overlap of neighbouring
+// output rows served from L2). One thread = one output pixel x all couts;
+// weights ([27][Cout], packed on the host) are wave-uniform scalar loads.
+constexpr int STEM_TW = 128;
+constexpr int STEM_SEG = 2 * STEM_TW + 16;  // staged columns per row segment (aligned window)
+
+template <typename T, int NC8>
+__global__ __launch_bounds__(STEM_TW) void conv_first(const FirstConvArgs p) {
+    __shared__ float patch[9][STEM_SEG];
+    const int wo0 = blockIdx.x * STEM_TW, ho = blockIdx.y, n = blockIdx.z;
     const T* x = reinterpret_cast<const T*>(p.io[0]);
     const long long plane = (long long)p.H * p.W;
-    const T* xn = x + (long long)n * 3 * plane;
-    float xv[27];
+    const int col0 = 2 * wo0 - 8;  // 16-B aligned window start (8 elements before the first tap)
+    constexpr int CPS = STEM_SEG / 8;
+    for (int c = threadIdx.x; c < 9 * CPS; c += STEM_TW) {
+        const int seg = c / CPS, ch = c - seg * CPS;
+        const int ci = seg / 3, kh = seg - ci * 3;
+        const int hi = 2 * ho - 1 + kh;
+        const int col = col0 + ch * 8;
+        float f[8];
+        if (hi >= 0 && hi < p.H && col >= 0 && col + 8 <= p.W) {
+            chunk_to_f(ld_chunk(x + ((long long)n * 3 + ci) * plane + (long long)hi * p.W + col), f);
+        } else {
 #pragma unroll
-    for (int ci = 0; ci < 3; ++ci)
-#pragma unroll
-        for (int kh = 0; kh < 3; ++kh) {
-            const int hi = ho * 2 - 1 + kh;
-#pragma unroll
-            for (int kw = 0; kw < 3; ++kw) {
-                const int wi = wo * 2 - 1 + kw;
-                float v = 0.f;
-                if (hi >= 0 && hi < p.H && wi >= 0 && wi < p.W) v = tof(xn[ci * plane + (long long)hi * p.W + wi]);
-                xv[ci * 9 + kh * 3 + kw] = v;
+            for (int e = 0; e < 8; ++e) {
+                const int cc = col + e;
+                f[e] = (hi >= 0 && hi < p.H && cc >= 0 && cc < p.W)
+                           ? tof(x[((long long)n * 3 + ci) * plane + (long long)hi * p.W + cc]) : 0.f;
             }
         }
-    T* out = reinterpret_cast<T*>(p.out) + (long long)m * p.ldo + co0;
 #pragma unroll
-    for (int c0 = 0; c0 < CPT; c0 += 8) {
+        for (int e = 0; e < 8; ++e) patch[seg][ch * 8 + e] = f[e];
+    }
+    __syncthreads();
+    const int wo = wo0 + threadIdx.x;
+    const bool live = wo < p.Wo;  // no early exit: keep the weight loads wave-uniform (scalar)
+    float xv[27];
+    const int lc = 2 * threadIdx.x - 1 + 8;  // local column of tap kw=0
+#pragma unroll
+    for (int seg = 0; seg < 9; ++seg)
+#pragma unroll
+        for (int kw = 0; kw < 3; ++kw) xv[seg * 3 + kw] = patch[seg][lc + kw];
+    const long long m = ((long long)n * p.Ho + ho) * p.Wo + wo;
+    T* out = reinterpret_cast<T*>(p.out) + m * p.ldo;
+    const float* __restrict__ wgt = p.w;
+    const float* __restrict__ bia = p.bias;
+    constexpr int COUT = NC8 * 8;
+#pragma unroll
+    for (int c0 = 0; c0 < COUT; c0 += 8) {
         float acc[8];
 #pragma unroll
-        for (int e = 0; e < 8; ++e) acc[e] = 0.f;
+        for (int e = 0; e < 8; ++e) acc[e] = bia[c0 + e];
 #pragma unroll
         for (int k = 0; k < 27; ++k) {
-            const float* wk = ws + k * p.Cout + co0 + c0;
 #pragma unroll
-            for (int e = 0; e < 8; ++e) acc[e] = fmaf(wk[e], xv[k], acc[e]);
+            for (int e = 0; e < 8; ++e) acc[e] = fmaf(wgt[k * COUT + c0 + e], xv[k], acc[e]);
         }
         float f[8];
 #pragma unroll
-        for (int e = 0; e < 8; ++e) {
-            float v = acc[e] + bs[co0 + c0 + e];
-            if (p.act == ACT_SILU) v = silu<T>(v);
-            f[e] = v;
+        for (int e = 0; e < 8; ++e) f[e] = p.act == ACT_SILU ? silu<T>(acc[e]) : acc[e];
+        if (live) st_chunk(out + c0, f_to_chunk<T>(f));
+    }
+}
+
+// 16-bit stem on MFMA: K = 27 taps padded to 32 = one v_mfma_f32_16x16x32 per
+// 16 pixels x 16 couts. A = weights (built once per wave from the fp32 [27][Cout]
+// pack), B = the im2col column of 16 pixels gathered from the LDS patch.
+template <typename T, int NT>
+__global__ __launch_bounds__(STEM_TW) void conv_first_mfma(const FirstConvArgs p) {
+    __shared__ float patch[9][STEM_SEG];
+    const int wo0 = blockIdx.x * STEM_TW, ho = blockIdx.y, n = blockIdx.z;
+    const T* x = reinterpret_cast<const T*>(p.io[0]);
+    const long long plane = (long long)p.H * p.W;
+    const int col0 = 2 * wo0 - 8;
+    constexpr int CPS = STEM_SEG / 8;
+    for (int c = threadIdx.x; c < 9 * CPS; c += STEM_TW) {
+        const int seg = c / CPS, ch = c - seg * CPS;
+        const int ci = seg / 3, kh = seg - ci * 3;
+        const int hi = 2 * ho - 1 + kh;
+        const int col = col0 + ch * 8;
+        float f[8];
+        if (hi >= 0 && hi < p.H && col >= 0 && col + 8 <= p.W) {
+            chunk_to_f(ld_chunk(x + ((long long)n * 3 + ci) * plane + (long long)hi * p.W + col), f);
+        } else {
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+                const int cc = col + e;
+                f[e] = (hi >= 0 && hi < p.H && cc >= 0 && cc < p.W)
+                           ? tof(x[((long long)n * 3 + ci) * plane + (long long)hi * p.W + cc]) : 0.f;
+            }
         }
-        st_chunk(out + c0, f_to_chunk<T>(f));
+#pragma unroll
+        for (int e = 0; e < 8; ++e) patch[seg][ch * 8 + e] = f[e];
+    }
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int fr = lane & 15, g = lane >> 4;
+    // A fragments: weights[cout = 16i + fr][k = 8g + j]
+    uint4 wf[NT];
+#pragma unroll
+    for (int i = 0; i < NT; ++i) {
+        float f[8];
+        const int co = 16 * i + fr;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const int k = 8 * g + j;
+            f[j] = (k < 27 && co < p.Cout) ? p.w[k * p.Cout + co] : 0.f;
+        }
+        wf[i] = f_to_chunk<T>(f).v[0];
+    }
+    float bv[NT][4];
+#pragma unroll
+    for (int i = 0; i < NT; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int co = 16 * i + 4 * g + r;
+            bv[i][r] = co < p.Cout ? p.bias[co] : 0.f;
+        }
+    __syncthreads();
+#pragma unroll
+    for (int pg = 0; pg < STEM_TW / 2 / 16; ++pg) {   // 4 groups of 16 pixels per wave
+        const int px = wave * (STEM_TW / 2) + pg * 16 + fr;
+        const int lc = 2 * px - 1 + 8;
+        float f[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const int k = 8 * g + j;
+            const int seg = k / 3, kw = k - seg * 3;
+            f[j] = k < 27 ? patch[seg][lc + kw] : 0.f;
+        }
+        const uint4 xf = f_to_chunk<T>(f).v[0];
+        const int wo = wo0 + px;
+        const long long m = ((long long)n * p.Ho + ho) * p.Wo + wo;
+        T* out = reinterpret_cast<T*>(p.out) + m * p.ldo;
+#pragma unroll
+        for (int i = 0; i < NT; ++i) {
+            f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+            Mma<T>::step(acc, &wf[i], &xf);
+            const int co = 16 * i + 4 * g;
+            if (wo < p.Wo && co < p.Cout) {
+                unsigned u[4];
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    float v = acc[r] + bv[i][r];
+                    if (p.act == ACT_SILU) v = silu<T>(v);
+                    u[r] = (unsigned short)__builtin_bit_cast(short, fromf<T>(v));
+                }
+                *reinterpret_cast<uint2*>(out + co) = make_uint2(u[0] | (u[1] << 16), u[2] | (u[3] << 16));
+            }
+        }
     }
 }
 
 template <typename T>
 int launch_first_t(const FirstConvArgs& a, int B, hipStream_t s) {
-    (void)B;
-    const dim3 blk(256);
-    if (a.Cout % 16 == 0) {
-        hipLaunchKernelGGL((conv_first<T, 16>), dim3((a.M + 255) / 256, a.Cout / 16), blk, 0, s, a);
-    } else {
-        hipLaunchKernelGGL((conv_first<T, 8>), dim3((a.M + 255) / 256, a.Cout / 8), blk, 0, s, a);
+    const dim3 grid((a.Wo + STEM_TW - 1) / STEM_TW, a.Ho, B);
+    if constexpr (sizeof(T) == 2) {
+        switch ((a.Cout + 15) / 16) {
+            case 1: hipLaunchKernelGGL((conv_first_mfma<T, 1>), grid, dim3(STEM_TW), 0, s, a); break;
+            case 2: hipLaunchKernelGGL((conv_first_mfma<T, 2>), grid, dim3(STEM_TW), 0, s, a); break;
+            case 4: hipLaunchKernelGGL((conv_first_mfma<T, 4>), grid, dim3(STEM_TW), 0, s, a); break;
+            case 6: hipLaunchKernelGGL((conv_first_mfma<T, 6>), grid, dim3(STEM_TW), 0, s, a); break;
+            default: return (int)hipErrorInvalidValue;
+        }
+        return (int)hipGetLastError();
+    }
+    switch (a.Cout) {
+        case 16: hipLaunchKernelGGL((conv_first<T, 2>), grid, dim3(STEM_TW), 0, s, a); break;
+        case 24: hipLaunchKernelGGL((conv_first<T, 3>), grid, dim3(STEM_TW), 0, s, a); break;
+        case 32: hipLaunchKernelGGL((conv_first<T, 4>), grid, dim3(STEM_TW), 0, s, a); break;
+        case 64: hipLaunchKernelGGL((conv_first<T, 8>), grid, dim3(STEM_TW), 0, s, a); break;
+        case 96: hipLaunchKernelGGL((conv_first<T, 12>), grid, dim3(STEM_TW), 0, s, a); break;
+        default: return (int)hipErrorInvalidValue;
     }
     return (int)hipGetLastError();
 }
@@ -360,11 +1004,53 @@ int conv_lds_bytes(int dtype, int BM, int BN, int Kp) {
     return (main_b > epi ? main_b : epi) + (Kp / 8) * 4;
 }
 
+template <typename T, int BM, int NS>
+int launch_stream_bn(int BN, const ConvArgs& a, hipStream_t s, int bpc) {
+    switch (BN) {
+        case 16: return launch_stream_t<T, BM, 16, NS>(a, s, bpc);
+        case 32: return launch_stream_t<T, BM, 32, NS>(a, s, bpc);
+        case 64: return launch_stream_t<T, BM, 64, NS>(a, s, bpc);
+        case 128: return launch_stream_t<T, BM, 128, (NS > 3 ? 3 : NS)>(a, s, bpc);
+    }
+    return (int)hipErrorInvalidValue;
+}
+
+template <typename T>
+int launch_stream(int BM, int BN, const ConvArgs& a, hipStream_t s) {
+    static const int ns = env_int("YH_SNS", 3);
+    static const int bpc_env = env_int("YH_SBPC", 0);
+    const int stage = (BM + BN) * 128;
+    const int lds = (ns > 3 && BN == 128 ? 3 : ns) * stage + 1024 + BM * (BN + 8) * 2 + a.Kp / 2 + a.gn * BN * 4;
+    int bpc = bpc_env > 0 ? bpc_env : (160 * 1024) / lds;
+    if (bpc < 1) bpc = 1;
+    if (bpc > 8) bpc = 8;
+    if (BM == 64) {
+        if (ns == 2) return launch_stream_bn<T, 64, 2>(BN, a, s, bpc);
+        if (ns == 4) return launch_stream_bn<T, 64, 4>(BN, a, s, bpc);
+        return launch_stream_bn<T, 64, 3>(BN, a, s, bpc);
+    }
+    if (ns == 2) return launch_stream_bn<T, 128, 2>(BN, a, s, bpc);
+    if (ns == 4) return launch_stream_bn<T, 128, 4>(BN, a, s, bpc);
+    return launch_stream_bn<T, 128, 3>(BN, a, s, bpc);
+}
+
 int launch_conv(int dtype, int BM, int BN, const ConvArgs& a, hipStream_t s) {
+    if (a.Kp % BK2 != 0) return (int)hipErrorInvalidValue;
+    static const int mode = env_int("YH_CONV", 0);
+    static const int sbm = env_int("YH_SBM", 64);
+    if (dtype != F32 && mode == 1) {
+        // persistent streaming kernel, grid from the tile count
+        ConvArgs b = a;
+        const int bm = sbm == 128 ? 128 : 64;
+        if (a.res && (bm / 64) * (BN / 8) * 64 / NT_ > 4) BN = 64;  // residual epilogue keeps <= 4 chunks per thread
+        b.gm = (a.M + bm - 1) / bm;
+        b.gn = (a.Cout + BN - 1) / BN;
+        return dtype == F16 ? launch_stream<_Float16>(bm, BN, b, s) : launch_stream<__bf16>(bm, BN, b, s);
+    }
     switch (dtype) {
         case F32: return launch_conv_bm<float>(BM, BN, a, s);
-        case F16: return launch_conv_bm<_Float16>(BM, BN, a, s);
-        case BF16: return launch_conv_bm<__bf16>(BM, BN, a, s);
+        case F16: return launch_conv2_bm<_Float16>(BM, BN, a, s);
+        case BF16: return launch_conv2_bm<__bf16>(BM, BN, a, s);
     }
     return (int)hipErrorInvalidValue;
 }

@@ -127,6 +127,7 @@ struct Net {
     std::vector<Op> ops;
     Workspace ws;
     void** io_dev = nullptr;      // {x, y}
+    void* zero_dev = nullptr;     // 256 zero bytes: source of padded conv taps
     bool use_graph = true;
     std::map<GraphKey, hipGraphExec_t> graphs;
     hipStream_t cap_stream = nullptr;
@@ -372,7 +373,7 @@ struct Net {
                 d.cin_p = 0;
                 for (auto& s : d.segs) d.cin_p += s.second;
                 d.K = d.k * d.k * d.cin_p;
-                d.Kp = round_up(d.K, 32);
+                d.Kp = round_up(d.K, 64);
                 d.cout_p = round_up(d.cout, 8);
                 d.coutp_pad = round_up(d.cout_p, 128);
             } else {
@@ -578,6 +579,7 @@ struct Net {
                 pick_tile(a.M, a.Cout, BM, BN);
                 a.gm = (a.M + BM - 1) / BM;
                 a.gn = (a.Cout + BN - 1) / BN;
+                a.zero = zero_dev;
                 rc = launch_conv(dtype, BM, BN, a, s);
                 break;
             }
@@ -765,6 +767,7 @@ struct Net {
         for (auto& d : convs) free_conv(d);
         if (ws.base) (void)hipFree(ws.base);
         if (io_dev) (void)hipFree(io_dev);
+        if (zero_dev) (void)hipFree(zero_dev);
         if (cap_stream) (void)hipStreamDestroy(cap_stream);
         for (auto e : ev) (void)hipEventDestroy(e);
     }
@@ -826,6 +829,8 @@ int yh_create(const yh_variant* v, int device, int dtype, yh_handle** out) {
         n.es = yh::dtype_size(dtype);
         n.build();
         HIPCHECK(hipMalloc(&n.io_dev, 2 * sizeof(void*)));
+        HIPCHECK(hipMalloc(&n.zero_dev, 256));
+        HIPCHECK(hipMemset(n.zero_dev, 0, 256));
         *out = h.release();
     });
 }
@@ -899,7 +904,7 @@ int yh_forward(yh_handle* h, const void* x, int batch, int height, int width, vo
 
 size_t yh_nms_workspace_bytes(int batch, int num_classes, int anchors) {
     if (batch <= 0 || num_classes <= 0 || anchors <= 0) return 0;
-    return (size_t)batch * anchors * num_classes * 8 + (size_t)batch * 4 + 256;
+    return (size_t)batch * anchors * num_classes * 8 + (size_t)batch * 4 + (size_t)batch * 2048 * 4 + 512;
 }
 
 int yh_nms(int dtype, const void* y, int batch, int num_classes, int anchors, float conf_threshold,
@@ -938,6 +943,13 @@ int yh_nms(int dtype, const void* y, int batch, int num_classes, int anchors, fl
         a.max_nms = max_nms;
         a.keys = (unsigned long long*)workspace;
         a.counts = (int*)((char*)workspace + (size_t)batch * anchors * num_classes * 8);
+        a.hist = (unsigned*)((char*)workspace + (((size_t)batch * anchors * num_classes * 8 + (size_t)batch * 4 + 255) & ~(size_t)255));
+        {   // lowest bin at the threshold (or 2047 bins below 1.0 for tiny thresholds)
+            uint32_t cb;
+            std::memcpy(&cb, &a.conf, 4);
+            const int one = 0x3F80;
+            a.bin_base = std::max((int)(cb >> 16), one - 2047);
+        }
         a.dets = dets;
         a.ndet = counts;
         const int rc = yh::launch_nms(dtype, a, (hipStream_t)stream);

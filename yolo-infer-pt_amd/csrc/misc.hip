@@ -170,11 +170,171 @@ __global__ __launch_bounds__(ATT_Q) void psa_attention(const AttnArgs p) {
     }
 }
 
+// ---------------------------------------------------------------------------
+// 16-bit attention on MFMA. One wave = 16 queries of one (image, head); keys in
+// blocks of 16:
+//   S^T = K_blk . Q^T        one v_mfma_f32_16x16x32 (dk = 32): A = K rows, B = Q rows,
+//                            both straight from the NHWC qkv buffer (16 B per lane);
+//                            the accumulator holds S^T[key 4g+r][query li] (g = lane/16).
+//   online softmax           per query = per lane column: in-lane max/sum over r plus two
+//                            xor-shuffles (16, 32); exact exp, fp32 state.
+//   O^T += V^T_blk . P^T     four v_mfma_f32_16x16x16 (dh = 64): B = P^T is exactly the
+//                            softmax'd accumulator of the S^T MFMA (no data movement),
+//                            A = V^T read from a per-wave LDS copy of V_blk with
+//                            ds_read_b64_tr_b16 (hardware transpose).
+// pe(v) (the depthwise positional conv, nets/nn.py:122) is added by pe_add below.
+typedef __attribute__((ext_vector_type(4))) short s16x4;
+typedef __attribute__((ext_vector_type(4))) _Float16 f16x4;
+
+template <typename T> struct Mma16;
+template <> struct Mma16<__bf16> {
+    static __device__ __forceinline__ f32x4 step(s16x4 a, s16x4 b, f32x4 c) {
+        return __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(a, b, c, 0, 0, 0);
+    }
+};
+template <> struct Mma16<_Float16> {
+    static __device__ __forceinline__ f32x4 step(s16x4 a, s16x4 b, f32x4 c) {
+        return __builtin_amdgcn_mfma_f32_16x16x16f16(__builtin_bit_cast(f16x4, a), __builtin_bit_cast(f16x4, b), c, 0, 0, 0);
+    }
+};
+
+__device__ __forceinline__ s16x4 lds_tr16(const void* p) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    typedef __attribute__((address_space(3))) s16x4* lp;
+    return __builtin_amdgcn_ds_read_tr16_b64_v4i16((lp)(const_cast<void*>(p)));
+#else
+    (void)p;
+    return s16x4{0, 0, 0, 0};
+#endif
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void psa_attention_mfma(const AttnArgs p) {
+    __shared__ __attribute__((aligned(16))) T vlds[4][16 * DH];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int q0 = (blockIdx.x * 4 + wave) * 16;
+    const int head = blockIdx.y, n = blockIdx.z;
+    if (q0 >= p.T) return;  // wave-uniform; the kernel has no block-level barrier
+    const int g = lane >> 4, li = lane & 15;
+    const T* base = reinterpret_cast<const T*>(p.qkv) + (long long)n * p.T * p.ldq + head * (2 * DK + DH);
+    const uint4 z4 = make_uint4(0, 0, 0, 0);
+    const int q = q0 + li;
+    const uint4 qf = q < p.T ? *reinterpret_cast<const uint4*>(base + (long long)q * p.ldq + 8 * g) : z4;
+    f32x4 o[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) o[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+    float mrun = -INFINITY, lrun = 0.f;
+    T* vl = vlds[wave];
+    for (int kb = 0; kb < p.T; kb += 16) {
+        const int key = kb + li;
+        const uint4 kf = key < p.T ? *reinterpret_cast<const uint4*>(base + (long long)key * p.ldq + DK + 8 * g) : z4;
+        uint4 vv[2];
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const int c = lane + 64 * h, kr = c >> 3, ch = c & 7;
+            vv[h] = (kb + kr < p.T) ? *reinterpret_cast<const uint4*>(base + (long long)(kb + kr) * p.ldq + 2 * DK + ch * 8) : z4;
+        }
+        f32x4 s = f32x4{0.f, 0.f, 0.f, 0.f};
+        Mma<T>::step(s, &kf, &qf);
+        float sv[4], mx = -INFINITY;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            sv[r] = (kb + 4 * g + r < p.T) ? s[r] * p.scale : -INFINITY;
+            mx = fmaxf(mx, sv[r]);
+        }
+        mx = fmaxf(mx, __shfl_xor(mx, 16));
+        mx = fmaxf(mx, __shfl_xor(mx, 32));
+        const float mnew = fmaxf(mrun, mx);
+        const float corr = __expf(mrun - mnew);
+        float ps = 0.f;
+        s16x4 pb;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const float pr = __expf(sv[r] - mnew);
+            pb[r] = __builtin_bit_cast(short, fromf<T>(pr));
+            ps += pr;
+        }
+        ps += __shfl_xor(ps, 16);
+        ps += __shfl_xor(ps, 32);
+        lrun = lrun * corr + ps;
+        mrun = mnew;
+#pragma unroll
+        for (int t = 0; t < 4; ++t) o[t] *= corr;
+        // V block -> LDS [16 keys][64 d]
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const int c = lane + 64 * h;
+            *reinterpret_cast<uint4*>(vl + (c >> 3) * DH + (c & 7) * 8) = vv[h];
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_wave_barrier();
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+            const s16x4 a = lds_tr16(vl + (4 * g + (li >> 2)) * DH + 16 * t + 4 * (li & 3));
+            o[t] = Mma16<T>::step(a, pb, o[t]);
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_wave_barrier();
+    }
+    if (q >= p.T) return;
+    const float inv = 1.0f / lrun;
+    T* out = reinterpret_cast<T*>(p.out) + ((long long)n * p.T + q) * p.ldo + head * DH;
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+        unsigned u[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) u[r] = (unsigned short)__builtin_bit_cast(short, fromf<T>(o[t][r] * inv));
+        *reinterpret_cast<uint2*>(out + 16 * t + 4 * g) = make_uint2(u[0] | (u[1] << 16), u[2] | (u[3] << 16));
+    }
+}
+
+// out[:, c] += pe_b[c] + sum_taps pe_w[tap][c] * v[nbr][c]   (c = head*dh + d; v lives in qkv)
+template <typename T>
+__global__ __launch_bounds__(256) void pe_add(const AttnArgs p, int B) {
+    const int C = p.heads * DH, cpp = C / 8;
+    const long long idx = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= (long long)B * p.T * cpp) return;
+    const int cc = (int)(idx % cpp);
+    const long long tok = idx / cpp;
+    const int n = (int)(tok / p.T), t = (int)(tok - (long long)n * p.T);
+    const int h = t / p.Ws, w = t - h * p.Ws;
+    const int c0 = cc * 8, head = c0 / DH, d0 = c0 - head * DH;
+    const T* vbase = reinterpret_cast<const T*>(p.qkv) + (long long)n * p.T * p.ldq + head * (2 * DK + DH) + 2 * DK + d0;
+    T* o = reinterpret_cast<T*>(p.out) + tok * p.ldo + c0;
+    float acc[8];
+    chunk_to_f(ld_chunk(o), acc);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) acc[e] += p.pe_b[c0 + e];
+#pragma unroll
+    for (int kh = 0; kh < 3; ++kh) {
+        const int hi = h - 1 + kh;
+        if (hi < 0 || hi >= p.Hs) continue;
+#pragma unroll
+        for (int kw = 0; kw < 3; ++kw) {
+            const int wi = w - 1 + kw;
+            if (wi < 0 || wi >= p.Ws) continue;
+            float f[8];
+            chunk_to_f(ld_chunk(vbase + (long long)(hi * p.Ws + wi) * p.ldq), f);
+            const float* wt = p.pe_w + (kh * 3 + kw) * C + c0;
+#pragma unroll
+            for (int e = 0; e < 8; ++e) acc[e] = fmaf(wt[e], f[e], acc[e]);
+        }
+    }
+    st_chunk(o, f_to_chunk<T>(acc));
+}
+
 template <typename T>
 int launch_attention_t(const AttnArgs& a, int B, hipStream_t s) {
     if (a.dk != DK || a.dh != DH) return (int)hipErrorInvalidValue;
-    const dim3 g((a.T + ATT_Q - 1) / ATT_Q, a.heads, B);
-    hipLaunchKernelGGL((psa_attention<T>), g, dim3(ATT_Q), 0, s, a);
+    if constexpr (sizeof(T) == 2) {
+        const dim3 g((a.T + 63) / 64, a.heads, B);
+        hipLaunchKernelGGL((psa_attention_mfma<T>), g, dim3(256), 0, s, a);
+        const long long n = (long long)B * a.T * (a.heads * DH / 8);
+        hipLaunchKernelGGL((pe_add<T>), dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, a, B);
+    } else {
+        const dim3 g((a.T + ATT_Q - 1) / ATT_Q, a.heads, B);
+        hipLaunchKernelGGL((psa_attention<T>), g, dim3(ATT_Q), 0, s, a);
+    }
     return (int)hipGetLastError();
 }
 

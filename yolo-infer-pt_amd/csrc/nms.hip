@@ -44,10 +44,19 @@ __device__ __forceinline__ unsigned long long make_key(float s, unsigned pair) {
     return ((unsigned long long)bits << PBITS) | (unsigned long long)(PMASK - pair);
 }
 
+constexpr int NBINS = 2048;  // coarse score bins = top 16 bits of the fp32 score, offset by the threshold's
+
+__device__ __forceinline__ int score_bin(float s, int base) {
+    const int b = (int)(__float_as_uint(s) >> 16) - base;
+    return b < 0 ? 0 : (b >= NBINS ? NBINS - 1 : b);
+}
+
 template <typename T>
 __global__ __launch_bounds__(256) void nms_emit(const NmsArgs p) {
     __shared__ int wtot[4];
     __shared__ int sbase;
+    __shared__ unsigned lhist[NBINS];
+    for (int i = threadIdx.x; i < NBINS; i += 256) lhist[i] = 0;
     const int n = blockIdx.y;
     const int a = blockIdx.x * 256 + threadIdx.x;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -71,9 +80,16 @@ __global__ __launch_bounds__(256) void nms_emit(const NmsArgs p) {
         unsigned long long* keys = p.keys + (long long)n * p.A * p.nc;
         for (int c = 0; c < p.nc; ++c) {
             const float s = tof(y[(long long)(4 + c) * p.A + a]);
-            if (s > p.conf) keys[off++] = make_key(s, (unsigned)(a * p.nc + c));
+            if (s > p.conf) {
+                keys[off++] = make_key(s, (unsigned)(a * p.nc + c));
+                atomicAdd(&lhist[score_bin(s, p.bin_base)], 1u);
+            }
         }
     }
+    __syncthreads();
+    unsigned* gh = p.hist + (long long)n * NBINS;
+    for (int i = threadIdx.x; i < NBINS; i += 256)
+        if (lhist[i]) atomicAdd(&gh[i], lhist[i]);
 }
 
 __device__ __forceinline__ bool iou_above(float ax1, float ay1, float ax2, float ay2, float aa,
@@ -87,7 +103,7 @@ __device__ __forceinline__ bool iou_above(float ax1, float ay1, float ax2, float
 }
 
 struct NmsSmem {
-    unsigned hist[HBINS];
+    unsigned hist[HBINS + 1];
     unsigned long long bkeys[CAP];
     float sb[SB][4];        // class-offset boxes of the sub-batch
     float sarea[SB];
@@ -106,118 +122,30 @@ struct NmsSmem {
 template <typename T>
 __device__ __forceinline__ float round_t(float v) { return tof(fromf<T>(v)); }
 
-template <typename T>
-__global__ __launch_bounds__(NMS_T) void nms_image(const NmsArgs p) {
-    extern __shared__ __attribute__((aligned(16))) char smem_raw[];
-    NmsSmem& S = *reinterpret_cast<NmsSmem*>(smem_raw);
-    const int n = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const T* y = reinterpret_cast<const T*>(p.y) + (long long)n * (4 + p.nc) * p.A;
-    const unsigned long long* keys = p.keys + (long long)n * p.A * p.nc;
-    float* dets = p.dets + (long long)n * p.max_det * 6;
-    const int nall = p.counts[n];
-    const int ktot = min(nall, p.max_nms);
-    if (tid == 0) S.kept = 0;
-    __syncthreads();
 
-    int processed = 0;
-    unsigned long long ub = ~0ull;  // every key < ub is still unprocessed
-    while (processed < ktot && S.kept < p.max_det) {
-        int want = min(CAP, ktot - processed);
-        const int remaining = nall - processed;
-        unsigned long long lo = 0;
-        if (remaining > want) {
-            // radix select: lo = want-th largest key below ub
-            unsigned long long prefix = 0;
-            int need = want;
-            for (int lvl = 0; lvl < 4; ++lvl) {
-                const int shift = 56 - DBITS * (lvl + 1);
-                for (int i = tid; i < HBINS; i += NMS_T) S.hist[i] = 0;
-                __syncthreads();
-                for (int i = tid; i < nall; i += NMS_T) {
-                    const unsigned long long k = keys[i];
-                    if (k < ub && (lvl == 0 || (k >> (shift + DBITS)) == prefix))
-                        atomicAdd(&S.hist[(k >> shift) & (HBINS - 1)], 1u);
-                }
-                __syncthreads();
-                // suffix scan over bins (bin HBINS-1 first): thread t owns bins [16t, 16t+16)
-                constexpr int PER = HBINS / NMS_T;
-                unsigned local = 0;
-#pragma unroll
-                for (int b = 0; b < PER; ++b) local += S.hist[tid * PER + b];
-                // hierarchical: suffix within wave via shuffles, wave totals in LDS
-                unsigned above = 0;  // keys in bins above this thread's range
-                unsigned v = local, incl = v;
-#pragma unroll
-                for (int d = 1; d < 64; d <<= 1) {
-                    const unsigned o = __shfl_down(incl, d);
-                    if (lane + d < 64) incl += o;
-                }
-                if (lane == 0) S.wsum[wave] = incl;  // incl at lane 0 = wave total
-                __syncthreads();
-                unsigned higher_waves = 0;
-                for (int w2 = wave + 1; w2 < NMS_T / 64; ++w2) higher_waves += S.wsum[w2];
-                above = higher_waves + (incl - v);
-                if (above < (unsigned)need && above + v >= (unsigned)need) {
-                    unsigned cum = above;
-                    for (int b = PER - 1; b >= 0; --b) {
-                        const unsigned h = S.hist[tid * PER + b];
-                        if (cum + h >= (unsigned)need) {
-                            S.sel_bin = tid * PER + b;
-                            S.sel_need = need - (int)cum;
-                            break;
-                        }
-                        cum += h;
-                    }
-                }
-                __syncthreads();
-                prefix = (prefix << DBITS) | (unsigned long long)S.sel_bin;
-                need = S.sel_need;
-                __syncthreads();
-            }
-            lo = prefix;
-        } else {
-            want = remaining;
-        }
-        // gather keys in [lo, ub) -> exactly `want` keys
-        if (tid == 0) S.gcount = 0;
-        __syncthreads();
-        for (int i0 = 0; i0 < nall; i0 += NMS_T) {
-            const int i = i0 + tid;
-            unsigned long long k = 0;
-            bool hit = false;
-            if (i < nall) { k = keys[i]; hit = k >= lo && k < ub; }
-            const unsigned long long bal = __ballot(hit);
-            if (bal) {
-                const int leader = __ffsll((long long)bal) - 1;
-                int base = 0;
-                if (lane == leader) base = atomicAdd(&S.gcount, __popcll(bal));
-                base = __shfl(base, leader);
-                if (hit) {
-                    const int pos = base + __popcll(bal & ((1ull << lane) - 1ull));
-                    if (pos < CAP) S.bkeys[pos] = k;
+__device__ void sort_batch(NmsSmem& S, int count, int tid) {
+    int P = 1;
+    while (P < count) P <<= 1;
+    for (int i = count + tid; i < P; i += NMS_T) S.bkeys[i] = 0;
+    __syncthreads();
+    for (int k = 2; k <= P; k <<= 1) {
+        for (int j = k >> 1; j > 0; j >>= 1) {
+            for (int i = tid; i < P; i += NMS_T) {
+                const int ixj = i ^ j;
+                if (ixj > i) {
+                    const unsigned long long a = S.bkeys[i], b = S.bkeys[ixj];
+                    const bool desc = (i & k) == 0;
+                    if (desc ? (a < b) : (a > b)) { S.bkeys[i] = b; S.bkeys[ixj] = a; }
                 }
             }
+            __syncthreads();
         }
-        __syncthreads();
-        int P = 1;
-        while (P < want) P <<= 1;
-        for (int i = want + tid; i < P; i += NMS_T) S.bkeys[i] = 0;
-        __syncthreads();
-        // bitonic sort, descending
-        for (int k = 2; k <= P; k <<= 1) {
-            for (int j = k >> 1; j > 0; j >>= 1) {
-                for (int i = tid; i < P; i += NMS_T) {
-                    const int ixj = i ^ j;
-                    if (ixj > i) {
-                        const unsigned long long a = S.bkeys[i], b = S.bkeys[ixj];
-                        const bool desc = (i & k) == 0;
-                        if (desc ? (a < b) : (a > b)) { S.bkeys[i] = b; S.bkeys[ixj] = a; }
-                    }
-                }
-                __syncthreads();
-            }
-        }
-        // greedy NMS over the sorted batch in sub-batches
+    }
+}
+
+// Greedy NMS over the first `want` keys of the sorted batch (sub-batches of SB).
+template <typename T>
+__device__ void nms_batch(NmsSmem& S, const NmsArgs& p, const T* y, float* dets, int want, int tid, int lane, int wave) {
         for (int s0 = 0; s0 < want && S.kept < p.max_det; s0 += SB) {
             const int ns = min(SB, want - s0);
             if (tid < ns) {
@@ -287,9 +215,204 @@ __global__ __launch_bounds__(NMS_T) void nms_image(const NmsArgs p) {
             }
             __syncthreads();
         }
-        processed += want;
-        ub = lo;
+}
+
+// block-wide inclusive scan of one value per thread (1024 threads)
+__device__ unsigned block_scan_incl(NmsSmem& S, unsigned v, int lane, int wave) {
+    unsigned incl = v;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const unsigned o = __shfl_up(incl, d);
+        if (lane >= d) incl += o;
+    }
+    if (lane == 63) S.wsum[wave] = incl;
+    __syncthreads();
+    unsigned before = 0;
+    for (int w = 0; w < wave; ++w) before += S.wsum[w];
+    __syncthreads();
+    return incl + before;
+}
+
+template <typename T>
+__global__ __launch_bounds__(NMS_T) void nms_image(const NmsArgs p) {
+    extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+    NmsSmem& S = *reinterpret_cast<NmsSmem*>(smem_raw);
+    const int n = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const T* y = reinterpret_cast<const T*>(p.y) + (long long)n * (4 + p.nc) * p.A;
+    const unsigned long long* keys = p.keys + (long long)n * p.A * p.nc;
+    float* dets = p.dets + (long long)n * p.max_det * 6;
+    const int nall = p.counts[n];
+    const int ktot = min(nall, p.max_nms);
+    if (tid == 0) S.kept = 0;
+
+    // C[b] = number of candidates in score bins >= b (suffix sums of the emitted histogram)
+    unsigned* C = S.hist;  // C[0..NBINS], C[NBINS] = 0
+    {
+        const unsigned* gh = p.hist + (long long)n * NBINS;
+        const int r0 = 2 * tid, r1 = 2 * tid + 1;  // reversed bin index: b = NBINS-1-r
+        const unsigned h0 = gh[NBINS - 1 - r0], h1 = gh[NBINS - 1 - r1];
+        const unsigned incl = block_scan_incl(S, h0 + h1, lane, wave);
+        C[NBINS - 1 - r1] = incl;
+        C[NBINS - 1 - r0] = incl - h1;
+        if (tid == 0) C[NBINS] = 0;
+    }
+    __syncthreads();
+
+    int processed = 0;
+    unsigned long long ub = ~0ull;  // every key < ub is still unprocessed
+    // ---- fast path: batches of whole score bins, ~1024..CAP keys, exact order by an LDS sort
+    int bin_hi = NBINS - 1;
+    bool fallback = false;
+    while (processed < ktot && S.kept < p.max_det && bin_hi >= 0) {
+        const unsigned c0 = C[bin_hi + 1];
+        const unsigned target = c0 + 1024u, cap = c0 + (unsigned)CAP;
+        if (tid == 0) {  // default: everything that is left fits the minimum batch
+            S.sel_bin = -1;
+            S.sel_need = (int)(C[0] - c0);
+        }
         __syncthreads();
+        if (C[0] >= target) {
+#pragma unroll
+            for (int e = 0; e < 2; ++e) {
+                const int b = 2 * tid + e;
+                if (b <= bin_hi && C[b + 1] < target && target <= C[b]) {
+                    if (C[b] <= cap) { S.sel_bin = b - 1; S.sel_need = (int)(C[b] - c0); }
+                    else { S.sel_bin = b; S.sel_need = (int)(C[b + 1] - c0); }
+                }
+            }
+        }
+        __syncthreads();
+        const int blo = S.sel_bin, bcnt = S.sel_need;
+        __syncthreads();
+        if (bcnt == 0) {
+            if (C[0] == c0) break;                        // every candidate processed
+            if (blo == bin_hi) { fallback = true; break; }  // one bin alone exceeds CAP
+            bin_hi = blo;                                 // skip empty bins
+            continue;
+        }
+        if (tid == 0) S.gcount = 0;
+        __syncthreads();
+        for (int i0 = 0; i0 < nall; i0 += NMS_T) {
+            const int i = i0 + tid;
+            unsigned long long k = 0;
+            bool hit = false;
+            if (i < nall) {
+                k = keys[i];
+                const int bb = score_bin(__uint_as_float((unsigned)(k >> PBITS)), p.bin_base);
+                hit = bb > blo && bb <= bin_hi;
+            }
+            const unsigned long long bal = __ballot(hit);
+            if (bal) {
+                const int leader = __ffsll((long long)bal) - 1;
+                int base = 0;
+                if (lane == leader) base = atomicAdd(&S.gcount, __popcll(bal));
+                base = __shfl(base, leader);
+                if (hit) {
+                    const int pos = base + __popcll(bal & ((1ull << lane) - 1ull));
+                    if (pos < CAP) S.bkeys[pos] = k;
+                }
+            }
+        }
+        __syncthreads();
+        const int want = min(bcnt, ktot - processed);
+        sort_batch(S, bcnt, tid);
+        nms_batch<T>(S, p, y, dets, want, tid, lane, wave);
+        processed += want;
+        ub = S.bkeys[want - 1];
+        bin_hi = blo;
+        __syncthreads();
+    }
+    if (fallback) {
+        // ---- general path: radix-select the next <= CAP keys below ub (exact for any ties)
+        while (processed < ktot && S.kept < p.max_det) {
+            int want = min(CAP, ktot - processed);
+            if (tid == 0) S.gcount = 0;
+            __syncthreads();
+            {
+                int c = 0;
+                for (int i = tid; i < nall; i += NMS_T) c += keys[i] < ub;
+                atomicAdd(&S.gcount, c);
+            }
+            __syncthreads();
+            const int remaining = S.gcount;
+            __syncthreads();
+            if (remaining == 0) break;
+            unsigned long long lo = 0;
+            if (remaining > want) {
+                unsigned long long prefix = 0;
+                int need = want;
+                for (int lvl = 0; lvl < 4; ++lvl) {
+                    const int shift = 56 - DBITS * (lvl + 1);
+                    for (int i = tid; i < HBINS; i += NMS_T) S.hist[i] = 0;
+                    __syncthreads();
+                    for (int i = tid; i < nall; i += NMS_T) {
+                        const unsigned long long k = keys[i];
+                        if (k < ub && (lvl == 0 || (k >> (shift + DBITS)) == prefix))
+                            atomicAdd(&S.hist[(k >> shift) & (HBINS - 1)], 1u);
+                    }
+                    __syncthreads();
+                    constexpr int PER = HBINS / NMS_T;
+                    unsigned local = 0;
+#pragma unroll
+                    for (int b = 0; b < PER; ++b) local += S.hist[tid * PER + b];
+                    unsigned incl = local;
+#pragma unroll
+                    for (int d = 1; d < 64; d <<= 1) {
+                        const unsigned o = __shfl_down(incl, d);
+                        if (lane + d < 64) incl += o;
+                    }
+                    if (lane == 0) S.wsum[wave] = incl;
+                    __syncthreads();
+                    unsigned above = 0;
+                    for (int w2 = wave + 1; w2 < NMS_T / 64; ++w2) above += S.wsum[w2];
+                    above += incl - local;
+                    if (above < (unsigned)need && above + local >= (unsigned)need) {
+                        unsigned cum = above;
+                        for (int b = PER - 1; b >= 0; --b) {
+                            const unsigned h = S.hist[tid * PER + b];
+                            if (cum + h >= (unsigned)need) {
+                                S.sel_bin = tid * PER + b;
+                                S.sel_need = need - (int)cum;
+                                break;
+                            }
+                            cum += h;
+                        }
+                    }
+                    __syncthreads();
+                    prefix = (prefix << DBITS) | (unsigned long long)S.sel_bin;
+                    need = S.sel_need;
+                    __syncthreads();
+                }
+                lo = prefix;
+            } else {
+                want = remaining;
+            }
+            if (tid == 0) S.gcount = 0;
+            __syncthreads();
+            for (int i0 = 0; i0 < nall; i0 += NMS_T) {
+                const int i = i0 + tid;
+                unsigned long long k = 0;
+                bool hit = false;
+                if (i < nall) { k = keys[i]; hit = k >= lo && k < ub; }
+                const unsigned long long bal = __ballot(hit);
+                if (bal) {
+                    const int leader = __ffsll((long long)bal) - 1;
+                    int base = 0;
+                    if (lane == leader) base = atomicAdd(&S.gcount, __popcll(bal));
+                    base = __shfl(base, leader);
+                    if (hit) {
+                        const int pos = base + __popcll(bal & ((1ull << lane) - 1ull));
+                        if (pos < CAP) S.bkeys[pos] = k;
+                    }
+                }
+            }
+            __syncthreads();
+            sort_batch(S, want, tid);
+            nms_batch<T>(S, p, y, dets, want, tid, lane, wave);
+            processed += want;
+            ub = lo;
+            __syncthreads();
+        }
     }
     if (tid == 0) p.ndet[n] = S.kept;
 }
@@ -297,6 +420,8 @@ __global__ __launch_bounds__(NMS_T) void nms_image(const NmsArgs p) {
 template <typename T>
 int launch_nms_t(const NmsArgs& a, hipStream_t s) {
     hipError_t e = hipMemsetAsync(a.counts, 0, sizeof(int) * a.B, s);
+    if (e != hipSuccess) return (int)e;
+    e = hipMemsetAsync(a.hist, 0, sizeof(unsigned) * NBINS * a.B, s);
     if (e != hipSuccess) return (int)e;
     hipLaunchKernelGGL((nms_emit<T>), dim3((a.A + 255) / 256, a.B), dim3(256), 0, s, a);
     static bool attr = false;
