@@ -133,6 +133,7 @@ def main():
     dtype = DTYPES[args.dtype]
 
     from yolo_hip import synth
+    from yolo_hip.dist import Gather
     from yolo_hip.engine import Engine, nms
 
     model = build_model(args.variant)
@@ -144,14 +145,13 @@ def main():
     x = synth.synth_scenes(B, S, S, seed=100 + rank).to(dev, dtype)
     A = eng.num_anchors(S, S)
     y = torch.empty((B, 84, A), dtype=dtype, device=dev)
-    gathered = [torch.empty((B, 300 * 6 + 1), device=dev) for _ in range(world)] if (dist and rank == 0) else None
+    gather = Gather(B, 300, dev, rank, world)
 
     def step():
         eng.forward(x, out=y)
         dets, counts = nms(y)
         if dist:
-            packed = torch.cat((dets.view(B, -1), counts.view(B, 1).float()), 1)
-            torch.distributed.gather(packed, gathered, dst=0)
+            gather(dets, counts)  # RCCL gather of the fixed-size results to rank 0
         return counts
 
     for _ in range(args.warmup):

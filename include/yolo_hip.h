@@ -156,6 +156,12 @@ int yh_op_info(const yh_handle* h, int index, int batch, int height, int width,
 /* Use a captured HIP graph for yh_forward (default on). */
 int yh_set_graph(yh_handle* h, int enable);
 
+/* Kernel that runs op `index` at (batch, height, width): for dense convs the
+ * implementation the per-shape tuner picked on the first yh_forward at that
+ * shape ("gemm", "gemm64", "gemm128", "stream", "direct"; all bit-identical),
+ * for the other ops the op's single kernel name. YH_ESTATE before that forward. */
+int yh_op_kernel(const yh_handle* h, int index, int batch, int height, int width, const char** name);
+
 #ifdef __cplusplus
 }
 #endif

@@ -55,12 +55,12 @@ def main():
         with open(os.environ["YH_PROF_OUT"], "w") as f:
             json.dump({"nms_us": e0.elapsed_time(e1) / steps * 1e3, "fwd_us": tot * 1e3,
                        "ops": [dict(label=o["label"], cls=o["cls"], us=o["ms"] / o["calls"] * 1e3,
-                                    bytes=o["bytes"], flops=o["flops"]) for o in ops]}, f)
+                                    bytes=o["bytes"], flops=o["flops"], kernel=o["kernel"]) for o in ops]}, f)
     rows = sorted(ops, key=lambda o: -o["ms"] / o["calls"])
     for o in rows:
         ms = o["ms"] / o["calls"]
         print(f"{ms * 1e3:8.1f} us {100 * ms / tot:5.1f}%  {o['bytes'] / ms / 1e6:7.0f} GB/s "
-              f"{o['flops'] / ms / 1e9:7.1f} TF/s  {o['bytes'] / 1e6:8.1f} MB  {o['cls']:9s} {o['label']}")
+              f"{o['flops'] / ms / 1e9:7.1f} TF/s  {o['bytes'] / 1e6:8.1f} MB  {o['cls']:9s} {o['kernel'] or '':9s} {o['label']}")
 
 
 if __name__ == "__main__":

@@ -91,8 +91,21 @@ struct NmsArgs {
     float* dets; int* ndet;
 };
 
+// Dense-conv kernels (16-bit types; F32 always runs conv_gemm). All of them
+// accumulate the K reduction in the same order (32-deep MFMA steps, increasing
+// k), so they produce bit-identical outputs and the engine may pick per layer.
+enum ConvKernel {
+    CONV_GEMM = 0,     // conv_gemm2, BM from the engine's tile heuristic
+    CONV_GEMM64 = 1,   // conv_gemm2, BM 64
+    CONV_GEMM128 = 2,  // conv_gemm2, BM 128
+    CONV_STREAM = 3,   // conv_stream, persistent BM 64 ring
+    CONV_DIRECT = 4,   // conv_direct, LDS-resident weights, register-streamed pixels
+    CONV_NKERNELS = 5
+};
+
 // launchers (return hipError_t as int)
-int launch_conv(int dtype, int BM, int BN, const ConvArgs& a, hipStream_t s);
+bool conv_kernel_ok(int dtype, int kern, const ConvArgs& a);
+int launch_conv(int dtype, int kern, int BM, int BN, const ConvArgs& a, hipStream_t s);
 int conv_lds_bytes(int dtype, int BM, int BN, int Kp);
 int launch_first_conv(int dtype, const FirstConvArgs& a, int B, hipStream_t s);
 int launch_dwconv(int dtype, const DwArgs& a, hipStream_t s);

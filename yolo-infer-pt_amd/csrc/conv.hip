@@ -20,11 +20,6 @@ namespace yh {
 
 namespace {
 
-int env_int(const char* name, int dflt) {
-    const char* e = getenv(name);
-    return e ? atoi(e) : dflt;
-}
-
 constexpr int BK = 32;        // reduction depth per stage (one 16x16x32 MFMA)
 constexpr int LDK = BK + 8;   // padded LDS row (elements) to spread banks
 constexpr int NT_ = 256;      // threads per block (4 waves)
@@ -702,6 +697,289 @@ int launch_stream_t(const ConvArgs& a, hipStream_t s, int blocks_per_cu) {
     return (int)hipGetLastError();
 }
 
+// ---------------------------------------------------------------------------
+// conv_direct: barrier-free implicit GEMM for the 16-bit types.
+//
+// A workgroup (8 waves) keeps one Cout slice of the packed weights resident in
+// LDS for its whole life and its waves stream pixel tiles independently: each
+// wave owns 16*MT output pixels x all BN couts of the slice, loads its pixel
+// operand (16 B of 8 channels per lane = one MFMA B-fragment) straight from
+// global memory into VGPRs D k-steps ahead of use, reads the weight fragments
+// from LDS and runs 16x16x32 MFMAs. There is no LDS staging of activations and
+// no barrier after the one-time weight fill, so latency is hidden by the
+// per-wave prefetch depth and by occupancy (4 waves/SIMD), not by block-wide
+// pipelining. The 3x3 halo re-reads (9 taps of each input pixel) are served by
+// L1/L2; HBM sees the input roughly once per Cout slice.
+//
+// Weight rows are permuted on the LDS fill so that the MFMA accumulator layout
+// (lane = pixel, 4 consecutive rows per lane quarter) lands 4*NTL *contiguous*
+// output channels in every lane: MFMA row (i, 4q + r) <- cout q*4*NTL + 4i + r.
+// The epilogue then stores straight from registers in 16-B chunks (bias, SiLU,
+// residual add in fp32), no LDS transpose.
+constexpr int DIRECT_WAVES = 8;
+constexpr int DIRECT_NT = DIRECT_WAVES * 64;
+constexpr int DIRECT_LDS_CAP = 80 * 1024;   // weight slice + ktab per block: 2 blocks per CU
+
+// KM: 0 = 1x1 stride 1 (two segments, nearest-up allowed); 1 = general kxk over
+// the k-table (one plain segment); 2 = 3x3 with Cin % 32 == 0, walked tap-major so
+// the tap's pixel address is computed once per tap, not once per 32-channel step.
+template <typename T, int NTL, int MT, int KM, int D>
+__global__ __launch_bounds__(DIRECT_NT, 2) void conv_direct(const ConvArgs p) {
+    constexpr bool K3 = KM != 0;
+    static_assert(sizeof(T) == 2, "16-bit path");
+    constexpr int BN = NTL * 16;   // D = k-steps in flight per wave
+    constexpr int RUN = 4 * NTL;  // contiguous couts per lane
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const int ldw = p.Kp * 2 + 16;                       // padded LDS row: conflict-free b128 reads
+    int* ktab = reinterpret_cast<int*>(smem + BN * ldw);
+    const int S = p.gn, PT = p.gm;
+    const int slice = blockIdx.x % S, bs = blockIdx.x / S, nbs = gridDim.x / S;
+    const int n0 = slice * BN;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int kc8 = p.Kp / 8;
+    {
+        const T* wg = reinterpret_cast<const T*>(p.w);
+        constexpr int FB = 8;   // loads in flight per thread during the fill
+        for (int c0 = tid; c0 < BN * kc8; c0 += DIRECT_NT * FB) {
+            // straight-line: out-of-range slots redo the last chunk (same value, same place)
+            uint4 v[FB];
+            int dst[FB];
+#pragma unroll
+            for (int u = 0; u < FB; ++u) {
+                const int c = min(c0 + u * DIRECT_NT, BN * kc8 - 1);
+                const int R = c / kc8, kc = c - R * kc8;
+                const int i = R >> 4, q = (R >> 2) & 3, r = R & 3;
+                const int co = n0 + q * RUN + 4 * i + r;
+                v[u] = *reinterpret_cast<const uint4*>(wg + (long long)co * p.Kp + kc * 8);
+                dst[u] = R * ldw + kc * 16;
+            }
+#pragma unroll
+            for (int u = 0; u < FB; ++u) *reinterpret_cast<uint4*>(smem + dst[u]) = v[u];
+        }
+        if constexpr (KM == 1)
+            for (int c = tid; c < kc8 + 8 * D; c += DIRECT_NT) ktab[c] = c < kc8 ? p.ktab[c] : 0xffff;
+    }
+    __syncthreads();
+
+    const int t_lo = (int)((long long)PT * bs / nbs), t_hi = (int)((long long)PT * (bs + 1) / nbs);
+    const int p16 = lane & 15, q = lane >> 4;
+    const int nks = (p.K + 31) / 32;
+    const int nkp = (nks + D - 1) / D * D;
+    const int kmax = p.Kp / 32 - 1;
+    const int HoWo = p.Ho * p.Wo;
+    const T* in0 = reinterpret_cast<const T*>(p.in0);
+    const T* in1 = reinterpret_cast<const T*>(p.in1);
+    const T* zero = reinterpret_cast<const T*>(p.zero);
+    const long long bs0 = (long long)p.h0 * p.w0 * p.ldc0;
+    const long long bs1 = (long long)p.h1 * p.w1 * p.ldc1;
+    const int co = n0 + q * RUN;   // this lane's first output channel
+    const char* wrow = smem + p16 * ldw + q * 16;
+
+    for (int t = t_lo + wave; t < t_hi; t += DIRECT_WAVES) {
+        const int m0 = t * 16 * MT;
+        // per-pixel loader state
+        int rn[MT], rhb[MT], rwb[MT];
+        const T* pb0[MT];
+        const T* pb1[MT];
+#pragma unroll
+        for (int j = 0; j < MT; ++j) {
+            const int m = m0 + j * 16 + p16;
+            const int mm = m < p.M ? m : p.M - 1;
+            const int n = mm / HoWo, rr = mm - n * HoWo;
+            const int ho = rr / p.Wo, wo = rr - ho * p.Wo;
+            rn[j] = m < p.M ? n : -1;
+            rhb[j] = m < p.M ? ho * p.stride - p.pad : -(1 << 20);   // out-of-range rows read the zero page
+            rwb[j] = wo * p.stride - p.pad;
+            if constexpr (K3) {
+                pb0[j] = in0 + n * bs0;
+                pb1[j] = nullptr;
+            } else {
+                pb0[j] = in0 + n * bs0 + ((long long)(ho >> p.up0) * p.w0 + (wo >> p.up0)) * p.ldc0;
+                pb1[j] = in1 + n * bs1 + ((long long)(ho >> p.up1) * p.w1 + (wo >> p.up1)) * p.ldc1 - p.c0;
+            }
+        }
+        // tap-major walk (KM == 2): wave-uniform (tap, 32-channel block) counters
+        int l_tap = 0, l_cb = 0;
+        const int ncb = p.Cin >> 5;
+        const T* tp[MT];
+        bool tv[MT];
+        auto set_tap = [&]() {
+            const int kh = l_tap / 3, kw = l_tap - kh * 3;
+#pragma unroll
+            for (int j = 0; j < MT; ++j) {
+                const int hi = rhb[j] + kh, wi = rwb[j] + kw;
+                tv[j] = (l_tap < 9) & ((unsigned)hi < (unsigned)p.Hi) & ((unsigned)wi < (unsigned)p.Wi);
+                tp[j] = pb0[j] + ((long long)hi * p.w0 + wi) * p.ldc0 + q * 8;
+            }
+        };
+        if constexpr (KM == 2) set_tap();
+        // Branch-free address selection (v_cndmask): a divergent branch here makes
+        // hipcc drain the loads in flight at the join.
+        auto load = [&](int ks, uint4 (&dst)[MT]) {
+            if constexpr (KM == 2) {
+#pragma unroll
+                for (int j = 0; j < MT; ++j)
+                    dst[j] = *reinterpret_cast<const uint4*>(tv[j] ? tp[j] + l_cb * 32 : zero);
+                if (++l_cb == ncb) {   // uniform: next tap
+                    l_cb = 0;
+                    ++l_tap;
+                    set_tap();
+                }
+            } else if constexpr (KM == 1) {
+                const int e = ktab[ks * 4 + q];   // padded with 0xffff past K
+                const int kh = e >> 24, kw = (e >> 16) & 0xff, ci = e & 0xffff;
+#pragma unroll
+                for (int j = 0; j < MT; ++j) {
+                    const int hi = rhb[j] + kh, wi = rwb[j] + kw;
+                    const bool ok = (ci != 0xffff) & ((unsigned)hi < (unsigned)p.Hi) & ((unsigned)wi < (unsigned)p.Wi);
+                    const T* src = pb0[j] + ((long long)hi * p.w0 + wi) * p.ldc0 + ci;
+                    dst[j] = *reinterpret_cast<const uint4*>(ok ? src : zero);
+                }
+            } else {
+                const int ci = ks * 32 + q * 8;
+                const bool in_k = ci < p.Cin, seg0 = ci < p.c0;
+#pragma unroll
+                for (int j = 0; j < MT; ++j) {
+                    const T* src = (seg0 ? pb0[j] : pb1[j]) + ci;
+                    dst[j] = *reinterpret_cast<const uint4*>((in_k && rn[j] >= 0) ? src : zero);
+                }
+            }
+        };
+
+        f32x4 acc[NTL][MT];
+#pragma unroll
+        for (int i = 0; i < NTL; ++i)
+#pragma unroll
+            for (int j = 0; j < MT; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+        uint4 buf[D][MT];
+#pragma unroll
+        for (int d = 0; d < D; ++d) load(d, buf[d]);
+        // The step count is padded to a multiple of D so the unrolled body has no
+        // branches (a skipped step would make hipcc drain the loads to avoid
+        // overwriting registers with loads still in flight). Padded steps read
+        // the zero page against a clamped (finite) weight row: they add 0.
+        for (int ks = 0; ks < nkp; ks += D) {
+#pragma unroll
+            for (int d = 0; d < D; ++d) {
+                const int kwr = min(ks + d, kmax);
+                uint4 wf[NTL];
+#pragma unroll
+                for (int i = 0; i < NTL; ++i)
+                    wf[i] = *reinterpret_cast<const uint4*>(wrow + i * 16 * ldw + kwr * 64);
+#pragma unroll
+                for (int j = 0; j < MT; ++j)
+#pragma unroll
+                    for (int i = 0; i < NTL; ++i) Mma<T>::step(acc[i][j], &wf[i], &buf[d][j]);
+                load(ks + d + D, buf[d]);
+            }
+        }
+
+        // epilogue: lane holds couts [co, co + RUN) of pixels m0 + j*16 + p16
+        if (co < p.Cout) {
+            float bv[RUN];
+#pragma unroll
+            for (int e = 0; e < RUN; ++e) bv[e] = p.bias[co + e];
+            const T* res = reinterpret_cast<const T*>(p.res);
+            T* out = reinterpret_cast<T*>(p.out);
+#pragma unroll
+            for (int j = 0; j < MT; ++j) {
+                const int m = m0 + j * 16 + p16;
+                if (m >= p.M) continue;
+                float v[RUN];
+#pragma unroll
+                for (int e = 0; e < RUN; ++e) {
+                    float x = acc[e >> 2][j][e & 3] + bv[e];
+                    if (p.act == ACT_SILU) x = silu<T>(x);
+                    v[e] = x;
+                }
+                if constexpr (RUN >= 8) {
+#pragma unroll
+                    for (int c8 = 0; c8 < RUN / 8; ++c8) {
+                        if (co + c8 * 8 >= p.Cout) break;
+                        float f[8];
+#pragma unroll
+                        for (int e = 0; e < 8; ++e) f[e] = fromf_round<T>(v[c8 * 8 + e]);
+                        if (res) {
+                            float g[8];
+                            chunk_to_f(ld_chunk(res + (long long)m * p.ldr + co + c8 * 8), g);
+#pragma unroll
+                            for (int e = 0; e < 8; ++e) f[e] += g[e];
+                        }
+                        st_chunk(out + (long long)m * p.ldo + co + c8 * 8, f_to_chunk<T>(f));
+                    }
+                } else {
+                    // RUN == 4: 8-byte store
+                    T o[4];
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) {
+                        float x = fromf_round<T>(v[e]);
+                        if (res) x += tof(res[(long long)m * p.ldr + co + e]);
+                        o[e] = fromf<T>(x);
+                    }
+                    *reinterpret_cast<uint2*>(out + (long long)m * p.ldo + co) = *reinterpret_cast<const uint2*>(o);
+                }
+            }
+        }
+    }
+}
+
+template <typename T, int NTL, int MT, int KM, int D>
+int launch_direct_t(const ConvArgs& a, int lds, int S, hipStream_t s) {
+    static bool attr_set = false;
+    if (!attr_set) {
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_direct<T, NTL, MT, KM, D>),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        attr_set = true;
+    }
+    ConvArgs b = a;
+    b.gn = S;
+    b.gm = (a.M + 16 * MT - 1) / (16 * MT);
+    // 2 blocks per CU, but never fewer than one pixel tile per wave
+    int nbs = (512 + S - 1) / S;
+    const int need = (b.gm + DIRECT_WAVES - 1) / DIRECT_WAVES;
+    if (nbs > need) nbs = need;
+    if (nbs < 1) nbs = 1;
+    hipLaunchKernelGGL((conv_direct<T, NTL, MT, KM, D>), dim3(nbs * S), dim3(DIRECT_NT), lds, s, b);
+    return (int)hipGetLastError();
+}
+
+// conv_direct plan: Cout slice width (16 * ntl) and LDS bytes; false when the
+// layer does not fit the kernel (3x3 over a concat / upsampled input, or a
+// weight slice beyond the LDS budget even at 16 couts).
+bool direct_plan(const ConvArgs& a, int* ntl_out, int* lds_out) {
+    const bool k1 = a.KH == 1 && a.KW == 1 && a.stride == 1 && a.pad == 0;
+    if (!k1 && (a.c1 != 0 || a.up0 != 0)) return false;
+    int ntl = a.Cout <= 16 ? 1 : a.Cout <= 32 ? 2 : 4;
+    auto lds_of = [&](int n) { return n * 16 * (a.Kp * 2 + 16) + (a.Kp / 8 + 32) * 4; };
+    while (ntl > 1 && lds_of(ntl) > DIRECT_LDS_CAP) ntl >>= 1;
+    if (lds_of(ntl) > DIRECT_LDS_CAP) return false;
+    if (ntl_out) *ntl_out = ntl;
+    if (lds_out) *lds_out = lds_of(ntl);
+    return true;
+}
+
+template <typename T>
+int launch_direct(const ConvArgs& a, hipStream_t s) {
+    int ntl = 0, lds = 0;
+    if (!direct_plan(a, &ntl, &lds)) return (int)hipErrorInvalidValue;
+    const bool k1 = a.KH == 1 && a.KW == 1 && a.stride == 1 && a.pad == 0;
+    const int S = (a.Cout + ntl * 16 - 1) / (ntl * 16);
+    const bool short_k = (a.K + 31) / 32 <= 2;
+    const bool tap_major = a.KH == 3 && a.KW == 3 && a.Cin % 32 == 0;
+#define YH_DIR(n)                                                                          \
+    if (k1) return short_k ? launch_direct_t<T, n, 2, 0, 2>(a, lds, S, s)                  \
+                           : launch_direct_t<T, n, 2, 0, 4>(a, lds, S, s);                 \
+    if (tap_major) return launch_direct_t<T, n, 2, 2, 4>(a, lds, S, s);                    \
+    return short_k ? launch_direct_t<T, n, 2, 1, 2>(a, lds, S, s)                          \
+                   : launch_direct_t<T, n, 2, 1, 4>(a, lds, S, s);
+    switch (ntl) {
+        case 1: YH_DIR(1)
+        case 2: YH_DIR(2)
+        default: YH_DIR(4)
+    }
+#undef YH_DIR
+}
+
 template <typename T, int BM, int BN>
 int launch_conv2_t(const ConvArgs& a, hipStream_t s) {
     using SM = Smem2<BM, BN>;
@@ -1016,41 +1294,45 @@ int launch_stream_bn(int BN, const ConvArgs& a, hipStream_t s, int bpc) {
 }
 
 template <typename T>
-int launch_stream(int BM, int BN, const ConvArgs& a, hipStream_t s) {
-    static const int ns = env_int("YH_SNS", 3);
-    static const int bpc_env = env_int("YH_SBPC", 0);
-    const int stage = (BM + BN) * 128;
-    const int lds = (ns > 3 && BN == 128 ? 3 : ns) * stage + 1024 + BM * (BN + 8) * 2 + a.Kp / 2 + a.gn * BN * 4;
-    int bpc = bpc_env > 0 ? bpc_env : (160 * 1024) / lds;
-    if (bpc < 1) bpc = 1;
-    if (bpc > 8) bpc = 8;
-    if (BM == 64) {
-        if (ns == 2) return launch_stream_bn<T, 64, 2>(BN, a, s, bpc);
-        if (ns == 4) return launch_stream_bn<T, 64, 4>(BN, a, s, bpc);
-        return launch_stream_bn<T, 64, 3>(BN, a, s, bpc);
-    }
-    if (ns == 2) return launch_stream_bn<T, 128, 2>(BN, a, s, bpc);
-    if (ns == 4) return launch_stream_bn<T, 128, 4>(BN, a, s, bpc);
-    return launch_stream_bn<T, 128, 3>(BN, a, s, bpc);
+int launch_stream(int BN, const ConvArgs& a, hipStream_t s) {
+    // BM 64, 2-slot ring: the configuration that won the (BM, ring depth, blocks/CU)
+    // sweep; blocks per CU from the LDS footprint
+    const int lds = 2 * (64 + BN) * 128 + 1024 + 64 * (BN + 8) * 2 + a.Kp / 2 + a.gn * BN * 4;
+    int bpc = (160 * 1024) / lds;
+    bpc = bpc < 1 ? 1 : bpc > 8 ? 8 : bpc;
+    return launch_stream_bn<T, 64, 2>(BN, a, s, bpc);
 }
 
-int launch_conv(int dtype, int BM, int BN, const ConvArgs& a, hipStream_t s) {
-    if (a.Kp % BK2 != 0) return (int)hipErrorInvalidValue;
-    static const int mode = env_int("YH_CONV", 0);
-    static const int sbm = env_int("YH_SBM", 64);
-    if (dtype != F32 && mode == 1) {
-        // persistent streaming kernel, grid from the tile count
-        ConvArgs b = a;
-        const int bm = sbm == 128 ? 128 : 64;
-        if (a.res && (bm / 64) * (BN / 8) * 64 / NT_ > 4) BN = 64;  // residual epilogue keeps <= 4 chunks per thread
-        b.gm = (a.M + bm - 1) / bm;
-        b.gn = (a.Cout + BN - 1) / BN;
-        return dtype == F16 ? launch_stream<_Float16>(bm, BN, b, s) : launch_stream<__bf16>(bm, BN, b, s);
-    }
-    switch (dtype) {
-        case F32: return launch_conv_bm<float>(BM, BN, a, s);
-        case F16: return launch_conv2_bm<_Float16>(BM, BN, a, s);
-        case BF16: return launch_conv2_bm<__bf16>(BM, BN, a, s);
+bool conv_kernel_ok(int dtype, int kern, const ConvArgs& a) {
+    if (a.Kp % BK2 != 0) return false;
+    if (dtype == F32) return kern == CONV_GEMM;
+    if (kern == CONV_DIRECT) return direct_plan(a, nullptr, nullptr);
+    return kern >= CONV_GEMM && kern <= CONV_STREAM;
+}
+
+int launch_conv(int dtype, int kern, int BM, int BN, const ConvArgs& a, hipStream_t s) {
+    if (!conv_kernel_ok(dtype, kern, a)) return (int)hipErrorInvalidValue;
+    if (dtype == F32) return launch_conv_bm<float>(BM, BN, a, s);
+    const bool h = dtype == F16;
+    switch (kern) {
+        case CONV_GEMM:
+            return h ? launch_conv2_bm<_Float16>(BM, BN, a, s) : launch_conv2_bm<__bf16>(BM, BN, a, s);
+        case CONV_GEMM64:
+        case CONV_GEMM128: {
+            ConvArgs b = a;
+            const int bm = kern == CONV_GEMM64 ? 64 : 128;
+            b.gm = (a.M + bm - 1) / bm;
+            return h ? launch_conv2_bm<_Float16>(bm, BN, b, s) : launch_conv2_bm<__bf16>(bm, BN, b, s);
+        }
+        case CONV_STREAM: {
+            ConvArgs b = a;
+            if (a.res && BN > 64) BN = 64;  // residual epilogue keeps <= 4 chunks per thread
+            b.gm = (a.M + 63) / 64;
+            b.gn = (a.Cout + BN - 1) / BN;
+            return h ? launch_stream<_Float16>(BN, b, s) : launch_stream<__bf16>(BN, b, s);
+        }
+        case CONV_DIRECT:
+            return h ? launch_direct<_Float16>(a, s) : launch_direct<__bf16>(a, s);
     }
     return (int)hipErrorInvalidValue;
 }

@@ -35,6 +35,8 @@ __device__ __forceinline__ Chunk<T> zero_chunk() {
 
 template <typename T> __device__ __forceinline__ float tof(T v) { return (float)v; }
 template <typename T> __device__ __forceinline__ T fromf(float v) { return (T)v; }
+// v rounded to T and back (the value a T store followed by a load would give)
+template <typename T> __device__ __forceinline__ float fromf_round(float v) { return tof(fromf<T>(v)); }
 
 template <typename T>
 __device__ __forceinline__ void chunk_to_f(const Chunk<T>& c, float (&f)[8]) {

@@ -136,6 +136,11 @@ struct Net {
     std::vector<int> prof_calls;
     std::vector<hipEvent_t> ev;
     int lastB = 0, lastH = 0, lastW = 0;
+    // per-shape choice of dense-conv kernel for every op (ConvKernel; CONV_GEMM for
+    // non-conv ops): timed once per (B, H, W) on the caller's stream, or forced by
+    // YH_CONV=<kernel id>
+    std::map<GraphKey, std::vector<int>> conv_kern;
+    const std::vector<int>* cur_kern = nullptr;
 
     // ---------------------------------------------------------- builder
     int tensor(int level, int C) {
@@ -533,6 +538,82 @@ struct Net {
         }
     }
 
+    void conv_args(const Op& op, int B, int H, int W, ConvArgs& a, int& BM, int& BN) const {
+        const ConvDesc& d = convs[op.conv];
+        const Tensor& to = tensors[op.out.t];
+        const int lvl_in = tensors[op.in[0].v.t].level - op.in[0].up;
+        a.Hi = H >> lvl_in; a.Wi = W >> lvl_in;
+        a.Ho = H >> to.level; a.Wo = W >> to.level;
+        a.stride = d.stride; a.pad = d.k / 2; a.KH = d.k; a.KW = d.k;
+        for (size_t si = 0; si < op.in.size(); ++si) {
+            const Seg& sg = op.in[si];
+            const Tensor& ts = tensors[sg.v.t];
+            const int hh = H >> ts.level, ww = W >> ts.level;
+            if (si == 0) { a.in0 = ptr(sg.v); a.ldc0 = ts.C; a.c0 = sg.v.C; a.up0 = sg.up; a.h0 = hh; a.w0 = ww; }
+            else { a.in1 = ptr(sg.v); a.ldc1 = ts.C; a.c1 = sg.v.C; a.up1 = sg.up; a.h1 = hh; a.w1 = ww; }
+        }
+        if (op.in.size() == 1) { a.in1 = a.in0; a.ldc1 = a.ldc0; a.c1 = 0; a.up1 = 0; a.h1 = a.h0; a.w1 = a.w0; }
+        a.Cin = d.cin_p; a.K = d.K; a.Kp = d.Kp;
+        a.M = B * a.Ho * a.Wo;
+        a.w = d.w_dev; a.bias = d.b_dev; a.ktab = d.ktab_dev;
+        a.out = ptr(op.out); a.ldo = to.C;
+        if (op.has_res) { a.res = ptr(op.res); a.ldr = ldc(op.res); }
+        a.Cout = d.cout_p;
+        a.act = d.act;
+        pick_tile(a.M, a.Cout, BM, BN);
+        a.gm = (a.M + BM - 1) / BM;
+        a.gn = (a.Cout + BN - 1) / BN;
+        a.zero = zero_dev;
+    }
+
+    // Pick the dense-conv kernel of every conv op for this shape: one plain forward
+    // (realistic activations in the workspace), then each candidate kernel of each
+    // conv timed over 3 launches after a warm-up launch. The candidates produce
+    // bit-identical outputs, so the choice only changes speed. Runs outside any
+    // graph capture; the caller's next forward recomputes every activation.
+    void ensure_tuned(int B, int H, int W, hipStream_t s) {
+        const GraphKey key{B, H, W};
+        auto it = conv_kern.find(key);
+        if (it != conv_kern.end()) { cur_kern = &it->second; return; }
+        std::vector<int> ch(ops.size(), CONV_GEMM);
+        static const int forced = [] { const char* e = getenv("YH_CONV"); return e ? atoi(e) : -1; }();
+        if (dtype != F32) {
+            cur_kern = nullptr;
+            std::vector<ConvArgs> args(ops.size());
+            std::vector<int> bms(ops.size()), bns(ops.size());
+            for (size_t i = 0; i < ops.size(); ++i)
+                if (ops[i].kind == OP_CONV) conv_args(ops[i], B, H, W, args[i], bms[i], bns[i]);
+            if (forced >= 0) {
+                for (size_t i = 0; i < ops.size(); ++i)
+                    if (ops[i].kind == OP_CONV && conv_kernel_ok(dtype, forced, args[i])) ch[i] = forced;
+            } else {
+                run_ops(B, H, W, s);
+                hipEvent_t e0, e1;
+                HIPCHECK(hipEventCreate(&e0));
+                HIPCHECK(hipEventCreate(&e1));
+                for (size_t i = 0; i < ops.size(); ++i) {
+                    if (ops[i].kind != OP_CONV) continue;
+                    float best = 1e30f;
+                    for (int k = 0; k < CONV_NKERNELS; ++k) {
+                        if (!conv_kernel_ok(dtype, k, args[i])) continue;
+                        int rc = launch_conv(dtype, k, bms[i], bns[i], args[i], s);
+                        HIPCHECK(hipEventRecord(e0, s));
+                        for (int r = 0; r < 3 && rc == 0; ++r) rc = launch_conv(dtype, k, bms[i], bns[i], args[i], s);
+                        HIPCHECK(hipEventRecord(e1, s));
+                        HIPCHECK(hipEventSynchronize(e1));
+                        if (rc != 0) throw Fail(YH_EHIP, "tuning launch of " + ops[i].label + " failed");
+                        float ms = 0.f;
+                        HIPCHECK(hipEventElapsedTime(&ms, e0, e1));
+                        if (ms < best) { best = ms; ch[i] = k; }
+                    }
+                }
+                (void)hipEventDestroy(e0);
+                (void)hipEventDestroy(e1);
+            }
+        }
+        cur_kern = &conv_kern.emplace(key, std::move(ch)).first->second;
+    }
+
     void launch_op(size_t oi, int B, int H, int W, hipStream_t s) {
         const Op& op = ops[oi];
         int rc = 0;
@@ -553,34 +634,11 @@ struct Net {
                 break;
             }
             case OP_CONV: {
-                const ConvDesc& d = convs[op.conv];
-                const Tensor& to = tensors[op.out.t];
                 ConvArgs a{};
-                const int lvl_in = tensors[op.in[0].v.t].level - op.in[0].up;
-                a.Hi = H >> lvl_in; a.Wi = W >> lvl_in;
-                a.Ho = H >> to.level; a.Wo = W >> to.level;
-                a.stride = d.stride; a.pad = d.k / 2; a.KH = d.k; a.KW = d.k;
-                for (size_t si = 0; si < op.in.size(); ++si) {
-                    const Seg& sg = op.in[si];
-                    const Tensor& ts = tensors[sg.v.t];
-                    const int hh = H >> ts.level, ww = W >> ts.level;
-                    if (si == 0) { a.in0 = ptr(sg.v); a.ldc0 = ts.C; a.c0 = sg.v.C; a.up0 = sg.up; a.h0 = hh; a.w0 = ww; }
-                    else { a.in1 = ptr(sg.v); a.ldc1 = ts.C; a.c1 = sg.v.C; a.up1 = sg.up; a.h1 = hh; a.w1 = ww; }
-                }
-                if (op.in.size() == 1) { a.in1 = a.in0; a.ldc1 = a.ldc0; a.c1 = 0; a.up1 = 0; a.h1 = a.h0; a.w1 = a.w0; }
-                a.Cin = d.cin_p; a.K = d.K; a.Kp = d.Kp;
-                a.M = B * a.Ho * a.Wo;
-                a.w = d.w_dev; a.bias = d.b_dev; a.ktab = d.ktab_dev;
-                a.out = ptr(op.out); a.ldo = to.C;
-                if (op.has_res) { a.res = ptr(op.res); a.ldr = ldc(op.res); }
-                a.Cout = d.cout_p;
-                a.act = d.act;
                 int BM, BN;
-                pick_tile(a.M, a.Cout, BM, BN);
-                a.gm = (a.M + BM - 1) / BM;
-                a.gn = (a.Cout + BN - 1) / BN;
-                a.zero = zero_dev;
-                rc = launch_conv(dtype, BM, BN, a, s);
+                conv_args(op, B, H, W, a, BM, BN);
+                const int kern = cur_kern ? (*cur_kern)[oi] : CONV_GEMM;
+                rc = launch_conv(dtype, kern, BM, BN, a, s);
                 break;
             }
             case OP_DW: {
@@ -643,6 +701,7 @@ struct Net {
         reserve(B, H, W);
         HIPCHECK(hipSetDevice(device));
         require(launch_set_io(io_dev, x, y, s) == 0, "set_io launch failed", YH_EHIP);
+        ensure_tuned(B, H, W, s);
         lastB = B; lastH = H; lastW = W;
         if (profile) {
             if (ev.size() < 2 * ops.size()) {
@@ -980,6 +1039,27 @@ int yh_profile_reset(yh_handle* h) {
 }
 
 int yh_op_count(const yh_handle* h) { return h ? (int)h->net.ops.size() : YH_EINVAL; }
+
+int yh_op_kernel(const yh_handle* h, int index, int batch, int height, int width, const char** name) {
+    return guarded([&] {
+        yh::require(h && index >= 0 && index < (int)h->net.ops.size(), "op index out of range");
+        const yh::Net& n = h->net;
+        static const char* conv_names[] = {"gemm", "gemm64", "gemm128", "stream", "direct"};
+        static const char* op_names[] = {"stem", "conv", "dwconv", "sppf", "attention", "decode"};
+        const yh::Op& op = n.ops[index];
+        if (op.kind != yh::OP_CONV) {
+            if (name) *name = op_names[(int)op.kind];
+            return;
+        }
+        if (n.dtype == yh::F32) {
+            if (name) *name = "gemm_f32";
+            return;
+        }
+        auto it = n.conv_kern.find(yh::GraphKey{batch, height, width});
+        yh::require(it != n.conv_kern.end(), "no forward has run at this shape yet", YH_ESTATE);
+        if (name) *name = conv_names[it->second[index]];
+    });
+}
 
 int yh_op_info(const yh_handle* h, int index, int batch, int height, int width, const char** label, int* op_class,
                double* bytes, double* flops, double* ms_total, int* calls) {

@@ -49,6 +49,7 @@ _PROTOS = {
     "yh_op_info": (c_int, [c_void_p, c_int, c_int, c_int, c_int, POINTER(c_char_p), POINTER(c_int),
                            POINTER(c_double), POINTER(c_double), POINTER(c_double), POINTER(c_int)]),
     "yh_set_graph": (c_int, [c_void_p, c_int]),
+    "yh_op_kernel": (c_int, [c_void_p, c_int, c_int, c_int, c_int, POINTER(c_char_p)]),
 }
 
 _lib = None

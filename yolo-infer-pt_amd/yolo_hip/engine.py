@@ -160,8 +160,11 @@ class Engine:
             b, f, ms, calls = c_double(), c_double(), c_double(), c_int()
             check(lib().yh_op_info(self._h, i, int(batch), int(height), int(width), byref(label), byref(cls),
                                    byref(b), byref(f), byref(ms), byref(calls)))
+            kname = c_char_p()
+            rc = lib().yh_op_kernel(self._h, i, int(batch), int(height), int(width), byref(kname))
             out.append(dict(label=label.value.decode(), cls=OP_CLASSES[cls.value], bytes=b.value,
-                            flops=f.value, ms=ms.value, calls=calls.value))
+                            flops=f.value, ms=ms.value, calls=calls.value,
+                            kernel=kname.value.decode() if rc == 0 else None))
         return out
 
 
