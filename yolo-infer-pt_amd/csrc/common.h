@@ -89,6 +89,7 @@ struct NmsArgs {
     unsigned* hist;            // [B][2048] coarse score-bin histogram (zeroed by the launcher)
     int bin_base;              // (fp32 bits >> 16) of the lowest bin
     float* dets; int* ndet;
+    unsigned long long* trace;  // optional [B][16] phase timestamps (s_memrealtime), nullptr = off
 };
 
 // Dense-conv kernels (16-bit types; F32 always runs conv_gemm). All of them

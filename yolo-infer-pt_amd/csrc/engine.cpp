@@ -966,6 +966,15 @@ size_t yh_nms_workspace_bytes(int batch, int num_classes, int anchors) {
     return (size_t)batch * anchors * num_classes * 8 + (size_t)batch * 4 + (size_t)batch * 2048 * 4 + 512;
 }
 
+// Debug hook (not part of the ABI header): yh_debug_nms_trace(buf) makes later
+// yh_nms calls record per-image phase timestamps into the device buffer buf
+// ([batch][16] u64, s_memrealtime ticks at 100 MHz); nullptr turns it off.
+static unsigned long long* nms_trace = nullptr;
+extern "C" int yh_debug_nms_trace(void* device_buf) {
+    nms_trace = (unsigned long long*)device_buf;
+    return 0;
+}
+
 int yh_nms(int dtype, const void* y, int batch, int num_classes, int anchors, float conf_threshold,
            double iou_threshold, int max_det, int max_nms, float max_wh, void* workspace, size_t workspace_bytes,
            float* dets, int* counts, void* stream) {
@@ -1000,6 +1009,7 @@ int yh_nms(int dtype, const void* y, int batch, int num_classes, int anchors, fl
         a.max_wh = max_wh;
         a.max_det = max_det;
         a.max_nms = max_nms;
+        a.trace = nms_trace;
         a.keys = (unsigned long long*)workspace;
         a.counts = (int*)((char*)workspace + (size_t)batch * anchors * num_classes * 8);
         a.hist = (unsigned*)((char*)workspace + (((size_t)batch * anchors * num_classes * 8 + (size_t)batch * 4 + 255) & ~(size_t)255));

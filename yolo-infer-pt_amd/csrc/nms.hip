@@ -51,6 +51,9 @@ __device__ __forceinline__ int score_bin(float s, int base) {
     return b < 0 ? 0 : (b >= NBINS ? NBINS - 1 : b);
 }
 
+// 8 consecutive anchors per thread: one 16-B load (f16/bf16) or two (f32) per class row.
+constexpr int EMIT_APT = 8;
+
 template <typename T>
 __global__ __launch_bounds__(256) void nms_emit(const NmsArgs p) {
     __shared__ int wtot[4];
@@ -58,12 +61,29 @@ __global__ __launch_bounds__(256) void nms_emit(const NmsArgs p) {
     __shared__ unsigned lhist[NBINS];
     for (int i = threadIdx.x; i < NBINS; i += 256) lhist[i] = 0;
     const int n = blockIdx.y;
-    const int a = blockIdx.x * 256 + threadIdx.x;
+    const int a0 = (blockIdx.x * 256 + threadIdx.x) * EMIT_APT;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const T* y = reinterpret_cast<const T*>(p.y) + (long long)n * (4 + p.nc) * p.A;
+    const bool full = a0 + EMIT_APT <= p.A && (p.A % EMIT_APT) == 0;
+    auto row = [&](int c, float (&v)[EMIT_APT]) {
+        const T* src = y + (long long)(4 + c) * p.A + a0;
+        if (full) {
+            chunk_to_f(ld_chunk(src), v);
+        } else {
+#pragma unroll
+            for (int e = 0; e < EMIT_APT; ++e) v[e] = a0 + e < p.A ? tof(src[e]) : -1.0f;
+        }
+    };
     int cnt = 0;
-    if (a < p.A)
-        for (int c = 0; c < p.nc; ++c) cnt += tof(y[(long long)(4 + c) * p.A + a]) > p.conf;
+    if (a0 < p.A) {
+#pragma unroll 4
+        for (int c = 0; c < p.nc; ++c) {
+            float v[EMIT_APT];
+            row(c, v);
+#pragma unroll
+            for (int e = 0; e < EMIT_APT; ++e) cnt += v[e] > p.conf;
+        }
+    }
     int incl = cnt;
 #pragma unroll
     for (int d = 1; d < 64; d <<= 1) {
@@ -76,13 +96,19 @@ __global__ __launch_bounds__(256) void nms_emit(const NmsArgs p) {
     __syncthreads();
     int off = sbase + incl - cnt;
     for (int w = 0; w < wave; ++w) off += wtot[w];
-    if (a < p.A && cnt) {
+    if (cnt) {
+        // keys in the reference's row-major (anchor, class) order are not needed:
+        // nms_image orders candidates by key, and the key carries the pair index
         unsigned long long* keys = p.keys + (long long)n * p.A * p.nc;
         for (int c = 0; c < p.nc; ++c) {
-            const float s = tof(y[(long long)(4 + c) * p.A + a]);
-            if (s > p.conf) {
-                keys[off++] = make_key(s, (unsigned)(a * p.nc + c));
-                atomicAdd(&lhist[score_bin(s, p.bin_base)], 1u);
+            float v[EMIT_APT];
+            row(c, v);
+#pragma unroll
+            for (int e = 0; e < EMIT_APT; ++e) {
+                if (v[e] > p.conf) {
+                    keys[off++] = make_key(v[e], (unsigned)((a0 + e) * p.nc + c));
+                    atomicAdd(&lhist[score_bin(v[e], p.bin_base)], 1u);
+                }
             }
         }
     }
@@ -92,14 +118,45 @@ __global__ __launch_bounds__(256) void nms_emit(const NmsArgs p) {
         if (lhist[i]) atomicAdd(&gh[i], lhist[i]);
 }
 
+// IoU test "RN(inter / union) > thr" (fp32 division, torchvision contract) without
+// the division. For thr >= 0 a pair without positive intersection never passes
+// (0 / union is +-0 or NaN). Otherwise, with union > 0 finite, RN(q) > t <=>
+// RN(q) >= t+ (next float) <=> q > m or (q == m and the tie rounds up to t+),
+// m = (t + t+) / 2. inter, union are floats and m has <= 25 significant bits,
+// so m * union is exact in double and the comparison is exact. Degenerate unions
+// (<= 0, inf, NaN) take the division.
+struct IouThr {
+    float t;
+    double m;
+    bool tie_up, nonneg;
+};
+
+__device__ __forceinline__ IouThr make_thr(float t) {
+    IouThr r;
+    r.t = t;
+    r.nonneg = t >= 0.0f && t < 3.0e38f;
+    const float tp = __uint_as_float(__float_as_uint(t) + 1u);   // next float above t (t >= 0)
+    r.m = ((double)t + (double)tp) * 0.5;
+    r.tie_up = (__float_as_uint(t) & 1u) != 0;                   // t odd -> tie goes to even t+
+    return r;
+}
+
 __device__ __forceinline__ bool iou_above(float ax1, float ay1, float ax2, float ay2, float aa,
-                                          float bx1, float by1, float bx2, float by2, float ba, float thr) {
+                                          float bx1, float by1, float bx2, float by2, float ba, const IouThr& th) {
     const float xx1 = fmaxf(ax1, bx1), yy1 = fmaxf(ay1, by1);
     const float xx2 = fminf(ax2, bx2), yy2 = fminf(ay2, by2);
     const float w = fmaxf(0.0f, xx2 - xx1), h = fmaxf(0.0f, yy2 - yy1);
     const float inter = w * h;
-    const float ovr = inter / (aa + ba - inter);
-    return ovr > thr;
+    const float uni = aa + ba - inter;
+    if (th.nonneg) {
+        if (!(inter > 0.0f)) return false;
+        if (uni > 0.0f && uni < 3.0e38f && inter < 3.0e38f) {
+            const double lhs = (double)inter, rhs = th.m * (double)uni;
+            return lhs > rhs || (lhs == rhs && th.tie_up);
+        }
+    }
+    const float ovr = inter / uni;
+    return ovr > th.t;
 }
 
 struct NmsSmem {
@@ -112,6 +169,8 @@ struct NmsSmem {
     float scls[SB];
     unsigned long long smask[SB][4];
     unsigned supp[SB / 32];
+    unsigned long long und[4], kep[4];   // parallel-resolve state (bit i = sub-batch entry i)
+    int nslow;
     float kb[MAXDET][4];
     float karea[MAXDET];
     unsigned wsum[NMS_T / 64];
@@ -123,29 +182,119 @@ template <typename T>
 __device__ __forceinline__ float round_t(float v) { return tof(fromf<T>(v)); }
 
 
-__device__ void sort_batch(NmsSmem& S, int count, int tid) {
-    int P = 1;
-    while (P < count) P <<= 1;
-    for (int i = count + tid; i < P; i += NMS_T) S.bkeys[i] = 0;
-    __syncthreads();
+// Bitonic sort (descending) of bkeys[0, count), count <= CAP, padded with zero
+// keys to a power of two P. The keys live in registers: wave w owns indices
+// [w*64E, (w+1)*64E), element e of lane l being index w*64E + e*64 + l
+// (E = P / NMS_T, at least 1). Compare-exchange partners i ^ j are then
+// reached by a lane shuffle (j < 64), inside the thread (j < 64E), or through
+// LDS with a workgroup barrier (larger j: 10 of the 66 stages at P = 2048).
+__device__ __forceinline__ unsigned long long shfl_xor64(unsigned long long v, int m) {
+    const unsigned lo = __shfl_xor((unsigned)v, m), hi = __shfl_xor((unsigned)(v >> 32), m);
+    return ((unsigned long long)hi << 32) | lo;
+}
+
+template <int E>
+__device__ void sort_regs(NmsSmem& S, int count, int P, int tid) {
+    const int lane = tid & 63, wave = tid >> 6;
+    const int base = wave * 64 * E;
+    const bool active = base < P;
+    unsigned long long v[E];
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+        const int i = base + e * 64 + lane;
+        v[e] = active && i < count ? S.bkeys[i] : 0ull;   // pad with the smallest key
+    }
     for (int k = 2; k <= P; k <<= 1) {
         for (int j = k >> 1; j > 0; j >>= 1) {
-            for (int i = tid; i < P; i += NMS_T) {
-                const int ixj = i ^ j;
-                if (ixj > i) {
-                    const unsigned long long a = S.bkeys[i], b = S.bkeys[ixj];
+            if (j < 64) {
+#pragma unroll
+                for (int e = 0; e < E; ++e) {
+                    const unsigned long long o = shfl_xor64(v[e], j);
+                    const int i = base + e * 64 + lane;
+                    const bool lower = (lane & j) == 0, desc = (i & k) == 0;
+                    const bool take_max = lower == desc;
+                    v[e] = take_max ? (v[e] > o ? v[e] : o) : (v[e] < o ? v[e] : o);
+                }
+            } else if (j < 64 * E) {
+                const int jj = j >> 6;
+#pragma unroll
+                for (int e = 0; e < E; ++e) {
+                    if (e & jj) continue;
+                    const int i = base + e * 64 + lane;
                     const bool desc = (i & k) == 0;
-                    if (desc ? (a < b) : (a > b)) { S.bkeys[i] = b; S.bkeys[ixj] = a; }
+                    const unsigned long long a = v[e], b = v[e | jj];
+                    const bool sw = desc ? (a < b) : (a > b);
+                    v[e] = sw ? b : a;
+                    v[e | jj] = sw ? a : b;
+                }
+            } else {
+                __syncthreads();   // previous LDS readers are done
+                if (active)
+#pragma unroll
+                    for (int e = 0; e < E; ++e) S.bkeys[base + e * 64 + lane] = v[e];
+                __syncthreads();
+                if (active) {
+#pragma unroll
+                    for (int e = 0; e < E; ++e) {
+                        const int i = base + e * 64 + lane;
+                        const unsigned long long o = S.bkeys[i ^ j];
+                        const bool lower = (i & j) == 0, desc = (i & k) == 0;
+                        const bool take_max = lower == desc;
+                        v[e] = take_max ? (v[e] > o ? v[e] : o) : (v[e] < o ? v[e] : o);
+                    }
                 }
             }
-            __syncthreads();
         }
     }
+    __syncthreads();
+    if (active)
+#pragma unroll
+        for (int e = 0; e < E; ++e) S.bkeys[base + e * 64 + lane] = v[e];
+    __syncthreads();
+}
+
+__device__ void sort_batch(NmsSmem& S, int count, int tid) {
+    int P = 64;
+    while (P < count) P <<= 1;
+    if (P <= NMS_T) sort_regs<1>(S, count, P, tid);
+    else if (P <= 2 * NMS_T) sort_regs<2>(S, count, P, tid);
+    else sort_regs<4>(S, count, P, tid);
 }
 
 // Greedy NMS over the first `want` keys of the sorted batch (sub-batches of SB).
+// Pair test without branches for the common case; degenerate unions (<= 0, inf,
+// NaN) are flagged and resolved by the division in a rare second pass.
+__device__ __forceinline__ bool iou_fast(float ax1, float ay1, float ax2, float ay2, float aa,
+                                         float bx1, float by1, float bx2, float by2, float ba,
+                                         const IouThr& th, bool& slow) {
+    const float xx1 = fmaxf(ax1, bx1), yy1 = fmaxf(ay1, by1);
+    const float xx2 = fminf(ax2, bx2), yy2 = fminf(ay2, by2);
+    const float w = fmaxf(0.0f, xx2 - xx1), h = fmaxf(0.0f, yy2 - yy1);
+    const float inter = w * h;
+    const float uni = aa + ba - inter;
+    const double lhs = (double)inter, rhs = th.m * (double)uni;
+    const bool pos = inter > 0.0f;
+    const bool good = (uni > 0.0f) & (uni < 3.0e38f) & (inter < 3.0e38f);
+    slow |= pos & !good;
+    return pos & good & ((lhs > rhs) | ((lhs == rhs) & th.tie_up));
+}
+
+// Greedy NMS over the first `want` keys of the sorted batch, in sub-batches of SB
+// entries (torchvision nms semantics, util.py:162-163):
+//   1. decode the sub-batch's boxes (wh2xy in the input dtype, class offset);
+//   2. flag entries suppressed by an already-kept box (4 threads per entry);
+//   3. lower-triangular IoU bitmask: bit j of row i <=> j < i and IoU(i, j) > thr;
+//   4. resolve the greedy order in parallel rounds: an undecided entry with a kept
+//      suppressor is removed, one whose suppressors are all decided (and none
+//      kept) is kept. The first undecided entry always resolves, so this ends;
+//      it equals the sequential greedy, and truncating to the first
+//      max_det - kept keeps equals stopping the greedy there.
 template <typename T>
 __device__ void nms_batch(NmsSmem& S, const NmsArgs& p, const T* y, float* dets, int want, int tid, int lane, int wave) {
+        const int n = blockIdx.x;
+        int sbi = 0;
+        const IouThr th = make_thr(p.iou);
+#define SB_MARK(k) do { if (p.trace && tid == 0 && sbi == 0) p.trace[n * 16 + (k)] = __builtin_amdgcn_s_memrealtime(); } while (0)
         for (int s0 = 0; s0 < want && S.kept < p.max_det; s0 += SB) {
             const int ns = min(SB, want - s0);
             if (tid < ns) {
@@ -166,55 +315,164 @@ __device__ void nms_batch(NmsSmem& S, const NmsArgs& p, const T* y, float* dets,
                 S.scls[tid] = (float)c;
             }
             if (tid < SB / 32) S.supp[tid] = 0;
+            if (tid == 0) S.nslow = 0;
             __syncthreads();
+            SB_MARK(12);
             const int kept0 = S.kept;
-            {   // suppressed by an already-kept box? 4 threads per entry
+            bool slow = !th.nonneg;
+            {   // 2. suppressed by an already-kept box? 4 threads per entry, 4 kept boxes per step
+                const int e = tid >> 2, part = tid & 3;
+                if (e < ns) {
+                    const float ex1 = S.sb[e][0], ey1 = S.sb[e][1], ex2 = S.sb[e][2], ey2 = S.sb[e][3], ea = S.sarea[e];
+                    bool sup = false;
+                    for (int k0 = 0; k0 < kept0 && !sup; k0 += 16) {
+#pragma unroll
+                        for (int u = 0; u < 4; ++u) {
+                            const int k = k0 + 4 * u + part;
+                            if (k < kept0)
+                                sup |= iou_fast(S.kb[k][0], S.kb[k][1], S.kb[k][2], S.kb[k][3], S.karea[k],
+                                                ex1, ey1, ex2, ey2, ea, th, slow);
+                        }
+                    }
+                    if (sup) atomicOr(&S.supp[e >> 5], 1u << (e & 31));
+                }
+            }
+            {   // 3. lower-triangular pairwise mask, 64 columns per thread
+                const int i = tid >> 2, wd = tid & 3;
+                unsigned long long m = 0;
+                if (i < ns && wd * 64 < i) {
+                    const float ix1 = S.sb[i][0], iy1 = S.sb[i][1], ix2 = S.sb[i][2], iy2 = S.sb[i][3], ia = S.sarea[i];
+#pragma unroll 8
+                    for (int jj = 0; jj < 64; ++jj) {
+                        const int j = wd * 64 + jj;
+                        const bool hit = iou_fast(ix1, iy1, ix2, iy2, ia, S.sb[j][0], S.sb[j][1], S.sb[j][2], S.sb[j][3],
+                                                  S.sarea[j], th, slow);
+                        m |= (unsigned long long)hit << jj;
+                    }
+                    const int lim = i - wd * 64;   // columns j < i only
+                    if (lim < 64) m &= (1ull << lim) - 1ull;
+                }
+                S.smask[i][wd] = m;
+            }
+            if (slow) atomicAdd(&S.nslow, 1);
+            __syncthreads();
+            if (S.nslow) {
+                // rare: degenerate unions somewhere in this sub-batch -> exact division path
                 const int e = tid >> 2, part = tid & 3;
                 if (e < ns) {
                     bool sup = false;
                     for (int k = part; k < kept0 && !sup; k += 4)
                         sup = iou_above(S.kb[k][0], S.kb[k][1], S.kb[k][2], S.kb[k][3], S.karea[k],
-                                        S.sb[e][0], S.sb[e][1], S.sb[e][2], S.sb[e][3], S.sarea[e], p.iou);
+                                        S.sb[e][0], S.sb[e][1], S.sb[e][2], S.sb[e][3], S.sarea[e], th);
                     if (sup) atomicOr(&S.supp[e >> 5], 1u << (e & 31));
                 }
-            }
-            {   // pairwise mask: bit j of row i set if j > i and IoU(i, j) > thr
-                const int i = tid >> 2, wd = tid & 3;
+                const int i = e, wd = part;
                 unsigned long long m = 0;
                 if (i < ns) {
-                    const float ix1 = S.sb[i][0], iy1 = S.sb[i][1], ix2 = S.sb[i][2], iy2 = S.sb[i][3], ia = S.sarea[i];
                     for (int jj = 0; jj < 64; ++jj) {
                         const int j = wd * 64 + jj;
-                        if (j > i && j < ns &&
-                            iou_above(ix1, iy1, ix2, iy2, ia, S.sb[j][0], S.sb[j][1], S.sb[j][2], S.sb[j][3], S.sarea[j], p.iou))
+                        if (j < i && iou_above(S.sb[i][0], S.sb[i][1], S.sb[i][2], S.sb[i][3], S.sarea[i],
+                                               S.sb[j][0], S.sb[j][1], S.sb[j][2], S.sb[j][3], S.sarea[j], th))
                             m |= 1ull << jj;
                     }
                 }
                 S.smask[i][wd] = m;
+                __syncthreads();
+            }
+            SB_MARK(13);
+            // 4. parallel rounds (waves 0..3, one entry per thread)
+            unsigned long long low[4] = {0ull, 0ull, 0ull, 0ull};
+            bool undec = false, iskept = false;
+            if (tid < SB) {
+#pragma unroll
+                for (int w = 0; w < 4; ++w) low[w] = S.smask[tid][w];
+                undec = tid < ns && !((S.supp[tid >> 5] >> (tid & 31)) & 1u);
+                const unsigned long long bu = __ballot(undec);
+                if (lane == 0) { S.und[wave] = bu; S.kep[wave] = 0ull; }
             }
             __syncthreads();
-            if (wave == 0) {
-                unsigned long long removed = 0;
-                if (lane < 4) removed = (unsigned long long)S.supp[2 * lane] | ((unsigned long long)S.supp[2 * lane + 1] << 32);
-                int kept = kept0;
-                for (int i = 0; i < ns && kept < p.max_det; ++i) {
-                    const unsigned long long rw = __shfl(removed, i >> 6);
-                    if ((rw >> (i & 63)) & 1ull) continue;
-                    if (lane < 4) {
-                        S.kb[kept][lane] = S.sb[i][lane];
-                        removed |= S.smask[i][lane];
-                    }
-                    if (lane == 0) S.karea[kept] = S.sarea[i];
-                    if (lane < 6) {
-                        const float v = lane < 4 ? S.sraw[i][lane] : (lane == 4 ? S.sscore[i] : S.scls[i]);
-                        dets[kept * 6 + lane] = v;
-                    }
-                    ++kept;
+            for (;;) {
+                unsigned long long U[4], K[4];
+#pragma unroll
+                for (int w = 0; w < 4; ++w) { U[w] = S.und[w]; K[w] = S.kep[w]; }
+                if ((U[0] | U[1] | U[2] | U[3]) == 0ull) break;
+                bool nk = false, nr = false;
+                if (undec) {
+                    const unsigned long long hk = (low[0] & K[0]) | (low[1] & K[1]) | (low[2] & K[2]) | (low[3] & K[3]);
+                    const unsigned long long hu = (low[0] & U[0]) | (low[1] & U[1]) | (low[2] & U[2]) | (low[3] & U[3]);
+                    nr = hk != 0ull;
+                    nk = !nr && hu == 0ull;
                 }
-                if (lane == 0) S.kept = kept;
+                __syncthreads();   // all reads of U, K done
+                if (tid < SB) {
+                    undec = undec && !nk && !nr;
+                    iskept = iskept || nk;
+                    const unsigned long long bu = __ballot(undec), bk = __ballot(iskept);
+                    if (lane == 0) { S.und[wave] = bu; S.kep[wave] = bk; }
+                }
+                __syncthreads();
+            }
+            SB_MARK(14);
+            {   // outputs: rank of each kept entry among this sub-batch's kept
+                unsigned long long K[4];
+#pragma unroll
+                for (int w = 0; w < 4; ++w) K[w] = S.kep[w];
+                const int budget = p.max_det - kept0;
+                const int total = __popcll(K[0]) + __popcll(K[1]) + __popcll(K[2]) + __popcll(K[3]);
+                if (tid < SB && iskept) {
+                    int r = 0;
+#pragma unroll
+                    for (int w = 0; w < 4; ++w)
+                        r += w < wave ? __popcll(K[w]) : (w == wave ? __popcll(K[w] & ((1ull << lane) - 1ull)) : 0);
+                    if (r < budget) {
+                        const int o = kept0 + r;
+                        S.kb[o][0] = S.sb[tid][0]; S.kb[o][1] = S.sb[tid][1];
+                        S.kb[o][2] = S.sb[tid][2]; S.kb[o][3] = S.sb[tid][3];
+                        S.karea[o] = S.sarea[tid];
+                        float* d = dets + o * 6;
+                        d[0] = S.sraw[tid][0]; d[1] = S.sraw[tid][1]; d[2] = S.sraw[tid][2]; d[3] = S.sraw[tid][3];
+                        d[4] = S.sscore[tid]; d[5] = S.scls[tid];
+                    }
+                }
+                __syncthreads();
+                if (tid == 0) S.kept = kept0 + min(total, budget);
             }
             __syncthreads();
+            SB_MARK(15);
+            ++sbi;
         }
+}
+
+// Append every key with pred(key) to bkeys (order irrelevant: the batch is sorted
+// next). GU loads per thread are in flight before any is consumed.
+template <typename Pred>
+__device__ __forceinline__ void gather_keys(NmsSmem& S, const unsigned long long* keys, int nall, int tid, int lane,
+                                            Pred pred) {
+    constexpr int GU = 8;
+    for (int i0 = 0; i0 < nall; i0 += NMS_T * GU) {
+        unsigned long long k[GU];
+#pragma unroll
+        for (int u = 0; u < GU; ++u) {
+            const int i = i0 + u * NMS_T + tid;
+            k[u] = i < nall ? keys[i] : 0ull;
+        }
+#pragma unroll
+        for (int u = 0; u < GU; ++u) {
+            const int i = i0 + u * NMS_T + tid;
+            const bool hit = i < nall && pred(k[u]);
+            const unsigned long long bal = __ballot(hit);
+            if (bal) {
+                const int leader = __ffsll((long long)bal) - 1;
+                int base = 0;
+                if (lane == leader) base = atomicAdd(&S.gcount, __popcll(bal));
+                base = __shfl(base, leader);
+                if (hit) {
+                    const int pos = base + __popcll(bal & ((1ull << lane) - 1ull));
+                    if (pos < CAP) S.bkeys[pos] = k[u];
+                }
+            }
+        }
+    }
 }
 
 // block-wide inclusive scan of one value per thread (1024 threads)
@@ -233,6 +491,11 @@ __device__ unsigned block_scan_incl(NmsSmem& S, unsigned v, int lane, int wave) 
     return incl + before;
 }
 
+#define NMS_MARK(k)                                                                       \
+    do {                                                                                  \
+        if (p.trace && tid == 0) p.trace[n * 16 + (k)] = __builtin_amdgcn_s_memrealtime(); \
+    } while (0)
+
 template <typename T>
 __global__ __launch_bounds__(NMS_T) void nms_image(const NmsArgs p) {
     extern __shared__ __attribute__((aligned(16))) char smem_raw[];
@@ -244,6 +507,8 @@ __global__ __launch_bounds__(NMS_T) void nms_image(const NmsArgs p) {
     const int nall = p.counts[n];
     const int ktot = min(nall, p.max_nms);
     if (tid == 0) S.kept = 0;
+    NMS_MARK(0);
+    if (p.trace && tid == 0) p.trace[n * 16 + 7] = __builtin_amdgcn_s_memtime();
 
     // C[b] = number of candidates in score bins >= b (suffix sums of the emitted histogram)
     unsigned* C = S.hist;  // C[0..NBINS], C[NBINS] = 0
@@ -257,6 +522,8 @@ __global__ __launch_bounds__(NMS_T) void nms_image(const NmsArgs p) {
         if (tid == 0) C[NBINS] = 0;
     }
     __syncthreads();
+    NMS_MARK(1);
+    int nbatch = 0;
 
     int processed = 0;
     unsigned long long ub = ~0ull;  // every key < ub is still unprocessed
@@ -265,7 +532,7 @@ __global__ __launch_bounds__(NMS_T) void nms_image(const NmsArgs p) {
     bool fallback = false;
     while (processed < ktot && S.kept < p.max_det && bin_hi >= 0) {
         const unsigned c0 = C[bin_hi + 1];
-        const unsigned target = c0 + 1024u, cap = c0 + (unsigned)CAP;
+        const unsigned target = c0 + 640u, cap = c0 + (unsigned)CAP;   // 640: typically one batch of P = 1024
         if (tid == 0) {  // default: everything that is left fits the minimum batch
             S.sel_bin = -1;
             S.sel_need = (int)(C[0] - c0);
@@ -292,36 +559,25 @@ __global__ __launch_bounds__(NMS_T) void nms_image(const NmsArgs p) {
         }
         if (tid == 0) S.gcount = 0;
         __syncthreads();
-        for (int i0 = 0; i0 < nall; i0 += NMS_T) {
-            const int i = i0 + tid;
-            unsigned long long k = 0;
-            bool hit = false;
-            if (i < nall) {
-                k = keys[i];
-                const int bb = score_bin(__uint_as_float((unsigned)(k >> PBITS)), p.bin_base);
-                hit = bb > blo && bb <= bin_hi;
-            }
-            const unsigned long long bal = __ballot(hit);
-            if (bal) {
-                const int leader = __ffsll((long long)bal) - 1;
-                int base = 0;
-                if (lane == leader) base = atomicAdd(&S.gcount, __popcll(bal));
-                base = __shfl(base, leader);
-                if (hit) {
-                    const int pos = base + __popcll(bal & ((1ull << lane) - 1ull));
-                    if (pos < CAP) S.bkeys[pos] = k;
-                }
-            }
-        }
+        gather_keys(S, keys, nall, tid, lane, [&](unsigned long long k) {
+            const int bb = score_bin(__uint_as_float((unsigned)(k >> PBITS)), p.bin_base);
+            return bb > blo && bb <= bin_hi;
+        });
         __syncthreads();
+        if (nbatch == 0) NMS_MARK(2);
         const int want = min(bcnt, ktot - processed);
         sort_batch(S, bcnt, tid);
+        if (nbatch == 0) NMS_MARK(3);
         nms_batch<T>(S, p, y, dets, want, tid, lane, wave);
+        if (nbatch == 0) NMS_MARK(4);
+        ++nbatch;
         processed += want;
         ub = S.bkeys[want - 1];
         bin_hi = blo;
         __syncthreads();
     }
+    NMS_MARK(5);
+    if (p.trace && tid == 0) { p.trace[n * 16 + 8] = nbatch; p.trace[n * 16 + 9] = processed; p.trace[n * 16 + 11] = nall; }
     if (fallback) {
         // ---- general path: radix-select the next <= CAP keys below ub (exact for any ties)
         while (processed < ktot && S.kept < p.max_det) {
@@ -389,23 +645,7 @@ __global__ __launch_bounds__(NMS_T) void nms_image(const NmsArgs p) {
             }
             if (tid == 0) S.gcount = 0;
             __syncthreads();
-            for (int i0 = 0; i0 < nall; i0 += NMS_T) {
-                const int i = i0 + tid;
-                unsigned long long k = 0;
-                bool hit = false;
-                if (i < nall) { k = keys[i]; hit = k >= lo && k < ub; }
-                const unsigned long long bal = __ballot(hit);
-                if (bal) {
-                    const int leader = __ffsll((long long)bal) - 1;
-                    int base = 0;
-                    if (lane == leader) base = atomicAdd(&S.gcount, __popcll(bal));
-                    base = __shfl(base, leader);
-                    if (hit) {
-                        const int pos = base + __popcll(bal & ((1ull << lane) - 1ull));
-                        if (pos < CAP) S.bkeys[pos] = k;
-                    }
-                }
-            }
+            gather_keys(S, keys, nall, tid, lane, [&](unsigned long long k) { return k >= lo && k < ub; });
             __syncthreads();
             sort_batch(S, want, tid);
             nms_batch<T>(S, p, y, dets, want, tid, lane, wave);
@@ -414,6 +654,8 @@ __global__ __launch_bounds__(NMS_T) void nms_image(const NmsArgs p) {
             __syncthreads();
         }
     }
+    NMS_MARK(6);
+    if (p.trace && tid == 0) p.trace[n * 16 + 10] = __builtin_amdgcn_s_memtime();
     if (tid == 0) p.ndet[n] = S.kept;
 }
 
@@ -423,7 +665,7 @@ int launch_nms_t(const NmsArgs& a, hipStream_t s) {
     if (e != hipSuccess) return (int)e;
     e = hipMemsetAsync(a.hist, 0, sizeof(unsigned) * NBINS * a.B, s);
     if (e != hipSuccess) return (int)e;
-    hipLaunchKernelGGL((nms_emit<T>), dim3((a.A + 255) / 256, a.B), dim3(256), 0, s, a);
+    hipLaunchKernelGGL((nms_emit<T>), dim3((a.A + 256 * EMIT_APT - 1) / (256 * EMIT_APT), a.B), dim3(256), 0, s, a);
     static bool attr = false;
     if (!attr) {
         (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&nms_image<T>),
