@@ -70,14 +70,32 @@ def roofline(eng, args, batch, prof_steps, x, y):
             f"attainable {100 * c['attain_ms'] / c['ms']:4.1f}%")
     dom = by_cls["conv3x3"]
     achieved = dom["bytes"] / dom["ms"] / 1e6  # GB/s
+    traffic, traffic_src = pmc_traffic("conv3x3")
     return dict(bound="hbm", achieved=round(achieved, 1), peak=HBM_PEAK_GBS, unit="GB/s",
-                frac=round(achieved / HBM_PEAK_GBS, 4), traffic=None,
-                kernel="conv_gemm, dense 3x3 convs (implicit-GEMM MFMA)",
+                frac=round(achieved / HBM_PEAK_GBS, 4), traffic=traffic, traffic_source=traffic_src,
+                kernel="dense 3x3 convs: conv_direct / conv_gemm2 / conv_stream implicit-GEMM MFMA, autotuned per layer",
                 launches_per_step=dom["launches"],
                 avg_launch_us=round(dom["ms"] * 1e3 / dom["launches"], 2),
                 algorithmic_bytes_per_launch=round(dom["bytes"] / dom["launches"]),
                 attainable_frac=round(dom["attain_ms"] / dom["ms"], 4),
                 forward_kernel_ms=round(total, 4))
+
+
+PMC_SUMMARY = os.path.join(ROOT, "profiles", "pmc_traffic_latest.json")
+
+
+def pmc_traffic(cls):
+    """HBM bytes per launch of kernel family `cls` from the committed rocprofv3 PMC summary
+    (FETCH_SIZE / WRITE_SIZE passes over tools/pmc_run.py, corrected per the gfx950 guide by
+    tools/pmc_traffic.py); bench.py cannot collect PMC counters from inside its own process."""
+    try:
+        with open(PMC_SUMMARY) as f:
+            rec = json.load(f)
+        fam = rec["family"][cls]
+        return round(fam["traffic_per_launch"]), (f"{os.path.relpath(PMC_SUMMARY, ROOT)}: {rec['source']}; "
+                                                  f"{rec['corrections']}; {fam['traffic_over_alg']:.2f}x algorithmic")
+    except (OSError, KeyError, ValueError):
+        return None, None
 
 
 def cpu_baseline(args, min_seconds=10.0, max_seconds=30.0):

@@ -1,0 +1,86 @@
+"""HBM traffic per conv launch from two rocprofv3 --pmc passes (FETCH_SIZE, WRITE_SIZE)
+of tools/pmc_run.py, mapped onto the engine's ops.
+
+  python tools/pmc_traffic.py <fetch_dir> <write_dir> <ops.json> [out.json]
+
+Corrections per MI355X_MICROARCH.md (HBM / rocprofv3 section):
+  * FETCH_SIZE and WRITE_SIZE are reported in KiB (x 1024);
+  * on gfx950 FETCH_SIZE counts half the bytes of a wide (16 B/lane) coalesced
+    streaming read, which is every read of these kernels: x 2;
+  * WRITE_SIZE is exact for 16-B-per-lane stores.
+Infinity-Cache hits are counted as fabric requests, so this is L2-miss traffic
+(an upper bound on HBM bytes).
+
+The last forward of the workload has exactly one conv-kernel dispatch per
+OP_CONV op, in op order: the last N conv dispatches are matched to the N conv ops.
+"""
+import csv
+import glob
+import json
+import os
+import re
+import sys
+
+CONV_RE = re.compile(r"conv_(direct|gemm2|gemm|stream)(<|I)")
+
+
+def dispatches(d, counter):
+    files = glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)
+    if not files:
+        raise SystemExit(f"no counter_collection.csv under {d}")
+    rows = {}
+    for fn in files:
+        with open(fn) as f:
+            for r in csv.DictReader(f):
+                if r.get("Counter_Name") != counter:
+                    continue
+                did = int(r["Dispatch_Id"])
+                rec = rows.setdefault(did, dict(name=r["Kernel_Name"], value=0.0))
+                rec["value"] += float(r["Counter_Value"])
+    return [rows[k] for k in sorted(rows)]
+
+
+def conv_values(d, counter, n):
+    rows = [r for r in dispatches(d, counter) if CONV_RE.search(r["name"])]
+    if len(rows) < n:
+        raise SystemExit(f"{counter}: {len(rows)} conv dispatches < {n} conv ops")
+    return rows[-n:]
+
+
+def main():
+    fetch_dir, write_dir, ops_json = sys.argv[1:4]
+    out = sys.argv[4] if len(sys.argv) > 4 else None
+    ops = json.load(open(ops_json))
+    conv_ops = [o for o in ops if o["cls"] in ("conv3x3", "conv1x1")]
+    n = len(conv_ops)
+    fr = conv_values(fetch_dir, "FETCH_SIZE", n)
+    wr = conv_values(write_dir, "WRITE_SIZE", n)
+    per_op = []
+    for o, f, w in zip(conv_ops, fr, wr):
+        rd = f["value"] * 1024 * 2
+        wb = w["value"] * 1024
+        per_op.append(dict(label=o["label"], cls=o["cls"], kernel=f["name"][:80], alg_bytes=o["bytes"],
+                           read_bytes=rd, write_bytes=wb, traffic=rd + wb, ratio=(rd + wb) / o["bytes"]))
+    fam = {}
+    for cls in ("conv3x3", "conv1x1"):
+        rows = [r for r in per_op if r["cls"] == cls]
+        if not rows:
+            continue
+        fam[cls] = dict(launches=len(rows),
+                        traffic_per_launch=sum(r["traffic"] for r in rows) / len(rows),
+                        alg_bytes_per_launch=sum(r["alg_bytes"] for r in rows) / len(rows),
+                        traffic_over_alg=sum(r["traffic"] for r in rows) / sum(r["alg_bytes"] for r in rows))
+    rec = dict(source="rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of tools/pmc_run.py",
+               corrections="KiB x1024; FETCH_SIZE x2 (gfx950 wide-read half count)", family=fam, ops=per_op)
+    for cls, v in fam.items():
+        print(f"{cls}: {v['launches']} launches, traffic {v['traffic_per_launch'] / 1e6:.2f} MB/launch vs "
+              f"algorithmic {v['alg_bytes_per_launch'] / 1e6:.2f} MB ({v['traffic_over_alg']:.2f}x)")
+    for r in sorted(per_op, key=lambda r: -r["traffic"])[:12]:
+        print(f"  {r['label']:28s} {r['traffic'] / 1e6:8.2f} MB  alg {r['alg_bytes'] / 1e6:8.2f} MB  {r['ratio']:.2f}x")
+    if out:
+        with open(out, "w") as f:
+            json.dump(rec, f, indent=1)
+
+
+if __name__ == "__main__":
+    main()
