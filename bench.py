@@ -4,6 +4,10 @@ BASELINE.json metric: images/sec at 640x640 batch 32, v11_n, 1/2/4/8 MI355X.
 A step = one pass of the hot path over one batch resident in HBM: the HIP
 forward (yh_forward, replayed as a HIP graph), the on-device NMS (yh_nms) and,
 for N > 1, the RCCL gather of the fixed-size detection buffers to rank 0.
+By default steps are pipelined over two streams (yolo_hip.pipeline): the NMS
+(+ gather) of batch k runs beside the forward of batch k+1; every batch still
+gets its full forward and NMS inside the timed region. --serial runs them back
+to back on one stream.
 Data-parallel: every rank processes its own batch of 32 (weak scaling).
 
   python bench.py [--gpus N] [--steps K] [--warmup W]
@@ -138,6 +142,8 @@ def main():
     ap.add_argument("--profile-steps", type=int, default=None)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-roofline", action="store_true")
+    ap.add_argument("--serial", action="store_true",
+                    help="run forward and NMS back to back on one stream (no batch-to-batch overlap)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -153,6 +159,7 @@ def main():
     from yolo_hip import synth
     from yolo_hip.dist import Gather
     from yolo_hip.engine import Engine, nms
+    from yolo_hip.pipeline import DetectPipeline
 
     model = build_model(args.variant)
     eng = Engine(*model._yh_arch, dev, dtype)
@@ -165,12 +172,18 @@ def main():
     y = torch.empty((B, 84, A), dtype=dtype, device=dev)
     gather = Gather(B, 300, dev, rank, world)
 
+    post = (lambda d, c: gather(d, c)) if dist else None  # RCCL gather of the fixed-size results to rank 0
+    pipe = DetectPipeline(eng, B, S, S, post=post)
+
     def step():
-        eng.forward(x, out=y)
-        dets, counts = nms(y)
-        if dist:
-            gather(dets, counts)  # RCCL gather of the fixed-size results to rank 0
-        return counts
+        if args.serial:
+            eng.forward(x, out=y)
+            dets, counts = nms(y)
+            if dist:
+                post(dets, counts)
+            return counts
+        # forward of this batch overlaps the NMS (+ gather) of the previous one
+        return pipe.submit(x)[1]
 
     for _ in range(args.warmup):
         step()
@@ -223,6 +236,7 @@ def main():
                        "parallelism": f"dp{world}", "nms": "on-device, conf 0.001, iou 0.65, max_det 300"},
             "roofline": roof,
             "cpu_baseline": cpu,
+            "schedule": "serial" if args.serial else "2-stream pipeline (forward k+1 overlaps NMS k)",
             "kept_last_step": kept[:4],
         }
         print(json.dumps(rec), flush=True)

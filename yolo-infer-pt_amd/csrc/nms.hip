@@ -12,9 +12,10 @@
 // there); no wall-clock cutoff (util.py:166-167 is dropped).
 //
 // Design (gfx950):
-//   nms_emit   grid (A/256, B): every pair above conf becomes a 56-bit key
-//              (score bits << 26 | (2^26-1 - pair)); larger key = earlier in the
-//              reference order. Block-scanned, one atomic per block.
+//   nms_emit   grid (A/256, B), 8 class groups per block: every pair above conf
+//              becomes a 56-bit key (score bits << 26 | (2^26-1 - pair)); larger
+//              key = earlier in the reference order. Block-scanned, one atomic
+//              per block, plus a 2048-bin score histogram per image.
 //   nms_image  one 1024-thread workgroup per image: repeatedly radix-selects the
 //              next <= 4096 keys (4 x 14-bit digit histograms in LDS), gathers and
 //              bitonic-sorts them in LDS, then runs greedy NMS on 256-key
@@ -51,8 +52,15 @@ __device__ __forceinline__ int score_bin(float s, int base) {
     return b < 0 ? 0 : (b >= NBINS ? NBINS - 1 : b);
 }
 
-// 8 consecutive anchors per thread: one 16-B load (f16/bf16) or two (f32) per class row.
-constexpr int EMIT_APT = 8;
+// Candidate emit: a block covers 256 anchors (32 chunks of 8 consecutive anchors,
+// one 16-B load per class row) x 8 class groups; thread (chunk, group) scans the
+// group's classes, remembers which (anchor, class) pairs pass in a bitmask, then
+// re-reads only rows with a passing pair (L1/L2 hits) to write their keys. Keys
+// go out unordered (nms_image orders by key; the key carries the pair index).
+constexpr int EMIT_APT = 8;            // anchors per thread (one 16-B chunk)
+constexpr int EMIT_CHUNKS = 32;        // anchor chunks per block
+constexpr int EMIT_GROUPS = 8;         // class groups per block
+constexpr int EMIT_MAXC = 16;          // classes per group covered by the pass mask
 
 template <typename T>
 __global__ __launch_bounds__(256) void nms_emit(const NmsArgs p) {
@@ -61,8 +69,11 @@ __global__ __launch_bounds__(256) void nms_emit(const NmsArgs p) {
     __shared__ unsigned lhist[NBINS];
     for (int i = threadIdx.x; i < NBINS; i += 256) lhist[i] = 0;
     const int n = blockIdx.y;
-    const int a0 = (blockIdx.x * 256 + threadIdx.x) * EMIT_APT;
+    const int chunk = threadIdx.x & (EMIT_CHUNKS - 1), grp = threadIdx.x / EMIT_CHUNKS;
+    const int a0 = (blockIdx.x * EMIT_CHUNKS + chunk) * EMIT_APT;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int cpg = (p.nc + EMIT_GROUPS - 1) / EMIT_GROUPS;
+    const int c_lo = grp * cpg, c_hi = min(p.nc, c_lo + cpg);
     const T* y = reinterpret_cast<const T*>(p.y) + (long long)n * (4 + p.nc) * p.A;
     const bool full = a0 + EMIT_APT <= p.A && (p.A % EMIT_APT) == 0;
     auto row = [&](int c, float (&v)[EMIT_APT]) {
@@ -75,13 +86,19 @@ __global__ __launch_bounds__(256) void nms_emit(const NmsArgs p) {
         }
     };
     int cnt = 0;
+    unsigned rows_hit = 0;   // bit i: class c_lo + i has a passing anchor (i < EMIT_MAXC)
     if (a0 < p.A) {
 #pragma unroll 4
-        for (int c = 0; c < p.nc; ++c) {
+        for (int c = c_lo; c < c_hi; ++c) {
             float v[EMIT_APT];
             row(c, v);
+            int k = 0;
 #pragma unroll
-            for (int e = 0; e < EMIT_APT; ++e) cnt += v[e] > p.conf;
+            for (int e = 0; e < EMIT_APT; ++e) k += v[e] > p.conf;
+            cnt += k;
+            const int i = c - c_lo;
+            if (k && i < EMIT_MAXC) rows_hit |= 1u << i;
+            else if (k) rows_hit |= 0x80000000u;   // a class past the mask: rescan those rows
         }
     }
     int incl = cnt;
@@ -97,10 +114,11 @@ __global__ __launch_bounds__(256) void nms_emit(const NmsArgs p) {
     int off = sbase + incl - cnt;
     for (int w = 0; w < wave; ++w) off += wtot[w];
     if (cnt) {
-        // keys in the reference's row-major (anchor, class) order are not needed:
-        // nms_image orders candidates by key, and the key carries the pair index
         unsigned long long* keys = p.keys + (long long)n * p.A * p.nc;
-        for (int c = 0; c < p.nc; ++c) {
+        for (int c = c_lo; c < c_hi; ++c) {
+            const int i = c - c_lo;
+            const bool hit = i < EMIT_MAXC ? (rows_hit >> i) & 1u : (rows_hit >> 31) & 1u;
+            if (!hit) continue;
             float v[EMIT_APT];
             row(c, v);
 #pragma unroll
@@ -116,6 +134,14 @@ __global__ __launch_bounds__(256) void nms_emit(const NmsArgs p) {
     unsigned* gh = p.hist + (long long)n * NBINS;
     for (int i = threadIdx.x; i < NBINS; i += 256)
         if (lhist[i]) atomicAdd(&gh[i], lhist[i]);
+}
+
+// Zeroes the per-image candidate counts and score histograms (one launch instead of
+// two memsets).
+__global__ __launch_bounds__(256) void nms_zero(int* counts, unsigned* hist, int B) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i < B * NBINS) hist[i] = 0u;
+    if (i < B) counts[i] = 0;
 }
 
 // IoU test "RN(inter / union) > thr" (fp32 division, torchvision contract) without
@@ -661,11 +687,9 @@ __global__ __launch_bounds__(NMS_T) void nms_image(const NmsArgs p) {
 
 template <typename T>
 int launch_nms_t(const NmsArgs& a, hipStream_t s) {
-    hipError_t e = hipMemsetAsync(a.counts, 0, sizeof(int) * a.B, s);
-    if (e != hipSuccess) return (int)e;
-    e = hipMemsetAsync(a.hist, 0, sizeof(unsigned) * NBINS * a.B, s);
-    if (e != hipSuccess) return (int)e;
-    hipLaunchKernelGGL((nms_emit<T>), dim3((a.A + 256 * EMIT_APT - 1) / (256 * EMIT_APT), a.B), dim3(256), 0, s, a);
+    hipLaunchKernelGGL(nms_zero, dim3((a.B * NBINS + 255) / 256), dim3(256), 0, s, a.counts, a.hist, a.B);
+    const int per_block = EMIT_CHUNKS * EMIT_APT;
+    hipLaunchKernelGGL((nms_emit<T>), dim3((a.A + per_block - 1) / per_block, a.B), dim3(256), 0, s, a);
     static bool attr = false;
     if (!attr) {
         (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&nms_image<T>),
