@@ -10,7 +10,7 @@ OUT := $(PKG)/yolo_hip/libyolo_hip.so
 OBJDIR := build/obj
 HIPFLAGS := --offload-arch=$(ARCH) -O3 -fPIC -std=c++17 -Iinclude -I$(SRC) \
             -fhip-fp32-correctly-rounded-divide-sqrt -Wno-unused-result
-OBJS := $(OBJDIR)/engine.o $(OBJDIR)/conv.o $(OBJDIR)/misc.o $(OBJDIR)/nms.o
+OBJS := $(OBJDIR)/engine.o $(OBJDIR)/conv.o $(OBJDIR)/misc.o $(OBJDIR)/nms.o $(OBJDIR)/level.o
 
 all: $(OUT)
 
@@ -24,6 +24,9 @@ $(OBJDIR)/conv.o: $(SRC)/conv.hip $(SRC)/common.h $(SRC)/dtypes.h | $(OBJDIR)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
 $(OBJDIR)/misc.o: $(SRC)/misc.hip $(SRC)/common.h $(SRC)/dtypes.h | $(OBJDIR)
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+$(OBJDIR)/level.o: $(SRC)/level.hip $(SRC)/common.h $(SRC)/dtypes.h | $(OBJDIR)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
 $(OBJDIR)/nms.o: $(SRC)/nms.hip $(SRC)/common.h $(SRC)/dtypes.h | $(OBJDIR)

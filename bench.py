@@ -56,7 +56,7 @@ def roofline(eng, args, batch, prof_steps, x, y):
     for _ in range(prof_steps):
         eng.forward(x, out=y)
     eng.profile(False)
-    ops = eng.ops(batch, args.size, args.size)
+    ops = eng.units(batch, args.size, args.size)   # launch units: one op, or a fused level program
     by_cls = {}
     for o in ops:
         c = by_cls.setdefault(o["cls"], dict(ms=0.0, bytes=0.0, flops=0.0, launches=0, attain_ms=0.0))
@@ -65,7 +65,7 @@ def roofline(eng, args, batch, prof_steps, x, y):
         c["bytes"] += o["bytes"]
         c["flops"] += o["flops"]
         c["launches"] += 1
-        peak_tf = MFMA_PEAK_TFLOPS[args.dtype] if o["cls"] in ("conv3x3", "conv1x1") else 157.3
+        peak_tf = MFMA_PEAK_TFLOPS[args.dtype] if o["cls"] in ("conv3x3", "conv1x1", "level") else 157.3
         c["attain_ms"] += max(o["bytes"] / (HBM_PEAK_GBS * 1e9), o["flops"] / (peak_tf * 1e12)) * 1e3
     total = sum(c["ms"] for c in by_cls.values())
     for k, c in sorted(by_cls.items(), key=lambda kv: -kv[1]["ms"]):

@@ -158,9 +158,34 @@ int yh_set_graph(yh_handle* h, int enable);
 
 /* Kernel that runs op `index` at (batch, height, width): for dense convs the
  * implementation the per-shape tuner picked on the first yh_forward at that
- * shape ("gemm", "gemm64", "gemm128", "stream", "direct"; all bit-identical),
- * for the other ops the op's single kernel name. YH_ESTATE before that forward. */
+ * shape ("gemm", "gemm64", "gemm128", "stream", "direct", "stream4",
+ * "stream8"; all bit-identical), for the other ops the op's single kernel name.
+ * YH_ESTATE before that forward. */
 int yh_op_kernel(const yh_handle* h, int index, int batch, int height, int width, const char** name);
+
+/* Force dense-conv kernel `kernel` (0..6, the order of the names above) on every
+ * conv that supports it (the others run "gemm"), or -1 to return to per-shape
+ * autotuning. Drops the tuned choices and captured graphs. Testing hook: every
+ * kernel must produce bit-identical outputs. */
+int yh_force_conv_kernel(yh_handle* h, int kernel);
+
+/* Launch units of the forward at (batch, height, width), known after the first
+ * yh_forward at that shape: a unit is one op's kernel(s), or a run of ops of the
+ * 40x40 / 20x20 levels fused into one level-program launch (is_level = 1).
+ * yh_unit_count returns the count (YH_ESTATE before that forward). With
+ * yh_profile_enable, ms_total / calls accumulate per unit. */
+int yh_unit_count(const yh_handle* h, int batch, int height, int width);
+int yh_unit_info(const yh_handle* h, int index, int batch, int height, int width, int* first_op,
+                 int* num_ops, int* is_level, double* ms_total, int* calls);
+
+/* Fuse the 40x40 / 20x20 levels into level programs (16-bit handles; default
+ * off, or on with YH_LEVEL=1; outputs are bit-identical either way). Drops
+ * graphs and tuning. */
+int yh_set_level_fusion(yh_handle* h, int enable);
+
+/* 0 when no level-program cluster barrier has timed out on this handle, 1 if
+ * one has (results of that forward are invalid), <0 on error. Synchronous. */
+int yh_level_status(const yh_handle* h);
 
 #ifdef __cplusplus
 }

@@ -47,20 +47,20 @@ def main():
     e1.record()
     torch.cuda.synchronize()
     print(f"nms: {e0.elapsed_time(e1) / steps * 1e3:.1f} us per batch of {B} (kept {counts.tolist()[:4]})")
-    ops = eng.ops(B, size, size)
-    tot = sum(o["ms"] / o["calls"] for o in ops)
-    print(f"v11_{v} {size}^2 B={B} {dt}: forward kernels {tot * 1e3:.1f} us")
+    units = eng.units(B, size, size)
+    tot = sum(u["ms"] / max(1, u["calls"]) for u in units)
+    print(f"v11_{v} {size}^2 B={B} {dt}: forward kernels {tot * 1e3:.1f} us in {len(units)} launch units")
     if os.environ.get("YH_PROF_OUT"):
         import json
         with open(os.environ["YH_PROF_OUT"], "w") as f:
             json.dump({"nms_us": e0.elapsed_time(e1) / steps * 1e3, "fwd_us": tot * 1e3,
-                       "ops": [dict(label=o["label"], cls=o["cls"], us=o["ms"] / o["calls"] * 1e3,
-                                    bytes=o["bytes"], flops=o["flops"], kernel=o["kernel"]) for o in ops]}, f)
-    rows = sorted(ops, key=lambda o: -o["ms"] / o["calls"])
-    for o in rows:
-        ms = o["ms"] / o["calls"]
-        print(f"{ms * 1e3:8.1f} us {100 * ms / tot:5.1f}%  {o['bytes'] / ms / 1e6:7.0f} GB/s "
-              f"{o['flops'] / ms / 1e9:7.1f} TF/s  {o['bytes'] / 1e6:8.1f} MB  {o['cls']:9s} {o['kernel'] or '':9s} {o['label']}")
+                       "ops": [dict(label=u["label"], cls=u["cls"], us=u["ms"] / max(1, u["calls"]) * 1e3,
+                                    bytes=u["bytes"], flops=u["flops"], kernel=u["kernel"]) for u in units]}, f)
+    rows = sorted(units, key=lambda u: -u["ms"] / max(1, u["calls"]))
+    for u in rows:
+        ms = u["ms"] / max(1, u["calls"])
+        print(f"{ms * 1e3:8.1f} us {100 * ms / tot:5.1f}%  {u['bytes'] / ms / 1e6:7.0f} GB/s "
+              f"{u['flops'] / ms / 1e9:7.1f} TF/s  {u['bytes'] / 1e6:8.1f} MB  {u['cls']:9s} {u['kernel'] or '':9s} {u['label']}")
 
 
 if __name__ == "__main__":

@@ -1288,25 +1288,43 @@ int launch_stream_bn(int BN, const ConvArgs& a, hipStream_t s, int bpc) {
         case 16: return launch_stream_t<T, BM, 16, NS>(a, s, bpc);
         case 32: return launch_stream_t<T, BM, 32, NS>(a, s, bpc);
         case 64: return launch_stream_t<T, BM, 64, NS>(a, s, bpc);
-        case 128: return launch_stream_t<T, BM, 128, (NS > 3 ? 3 : NS)>(a, s, bpc);
+        case 128: return launch_stream_t<T, BM, 128, (NS > 4 ? 4 : NS)>(a, s, bpc);
     }
     return (int)hipErrorInvalidValue;
 }
 
+// BM 64. NS = 2 (the ring depth that wins on large layers: more blocks per CU)
+// or a deep ring (NS = 4 / 8: NS-1 stages in flight, for the small 20x20 /
+// 40x40 layers whose few tiles leave CUs idle and whose K loop is latency-bound).
+// Blocks per CU from the LDS footprint.
 template <typename T>
-int launch_stream(int BN, const ConvArgs& a, hipStream_t s) {
-    // BM 64, 2-slot ring: the configuration that won the (BM, ring depth, blocks/CU)
-    // sweep; blocks per CU from the LDS footprint
-    const int lds = 2 * (64 + BN) * 128 + 1024 + 64 * (BN + 8) * 2 + a.Kp / 2 + a.gn * BN * 4;
+int launch_stream(int BN, int NS, const ConvArgs& a, hipStream_t s) {
+    const int ns = (BN == 128 && NS > 4) ? 4 : NS;
+    const int lds = ns * (64 + BN) * 128 + 1024 + 64 * (BN + 8) * 2 + a.Kp / 2 + a.gn * BN * 4;
+    if (lds > 160 * 1024) return (int)hipErrorInvalidValue;
     int bpc = (160 * 1024) / lds;
     bpc = bpc < 1 ? 1 : bpc > 8 ? 8 : bpc;
-    return launch_stream_bn<T, 64, 2>(BN, a, s, bpc);
+    switch (NS) {
+        case 2: return launch_stream_bn<T, 64, 2>(BN, a, s, bpc);
+        case 4: return launch_stream_bn<T, 64, 4>(BN, a, s, bpc);
+        case 8: return launch_stream_bn<T, 64, 8>(BN, a, s, bpc);
+    }
+    return (int)hipErrorInvalidValue;
 }
 
 bool conv_kernel_ok(int dtype, int kern, const ConvArgs& a) {
     if (a.Kp % BK2 != 0) return false;
     if (dtype == F32) return kern == CONV_GEMM;
     if (kern == CONV_DIRECT) return direct_plan(a, nullptr, nullptr);
+    if (kern == CONV_STREAM4 || kern == CONV_STREAM8) {
+        // deep rings only pay off while the tiles leave CUs idle; LDS must fit
+        const int BN = a.Cout <= 16 ? 16 : a.Cout <= 32 ? 32 : a.Cout <= 64 ? 64 : 128;
+        const int ns = kern == CONV_STREAM4 ? 4 : (BN == 128 ? 4 : 8);
+        if (kern == CONV_STREAM8 && BN == 128) return false;
+        if (a.res && BN > 64) return false;
+        const int lds = ns * (64 + BN) * 128 + 1024 + 64 * (BN + 8) * 2 + a.Kp / 2 + ((a.Cout + BN - 1) / BN) * BN * 4;
+        return lds <= 160 * 1024 && a.Kp / BK2 >= 2;
+    }
     return kern >= CONV_GEMM && kern <= CONV_STREAM;
 }
 
@@ -1324,12 +1342,15 @@ int launch_conv(int dtype, int kern, int BM, int BN, const ConvArgs& a, hipStrea
             b.gm = (a.M + bm - 1) / bm;
             return h ? launch_conv2_bm<_Float16>(bm, BN, b, s) : launch_conv2_bm<__bf16>(bm, BN, b, s);
         }
-        case CONV_STREAM: {
+        case CONV_STREAM:
+        case CONV_STREAM4:
+        case CONV_STREAM8: {
             ConvArgs b = a;
             if (a.res && BN > 64) BN = 64;  // residual epilogue keeps <= 4 chunks per thread
             b.gm = (a.M + 63) / 64;
             b.gn = (a.Cout + BN - 1) / BN;
-            return h ? launch_stream<_Float16>(BN, b, s) : launch_stream<__bf16>(BN, b, s);
+            const int ns = kern == CONV_STREAM ? 2 : kern == CONV_STREAM4 ? 4 : 8;
+            return h ? launch_stream<_Float16>(BN, ns, b, s) : launch_stream<__bf16>(BN, ns, b, s);
         }
         case CONV_DIRECT:
             return h ? launch_direct<_Float16>(a, s) : launch_direct<__bf16>(a, s);

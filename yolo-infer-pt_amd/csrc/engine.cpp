@@ -19,6 +19,8 @@
 #include "common.h"
 #include "yolo_hip.h"
 
+static unsigned long long* level_trace_ptr = nullptr;   // yh_debug_level_trace
+
 namespace yh {
 
 static thread_local std::string g_err;
@@ -132,8 +134,9 @@ struct Net {
     std::map<GraphKey, hipGraphExec_t> graphs;
     hipStream_t cap_stream = nullptr;
     bool profile = false;
-    std::vector<double> prof_ms;
+    std::vector<double> prof_ms;     // per launch unit of the profiled shape
     std::vector<int> prof_calls;
+    GraphKey prof_key{0, 0, 0};
     std::vector<hipEvent_t> ev;
     int lastB = 0, lastH = 0, lastW = 0;
     // per-shape choice of dense-conv kernel for every op (ConvKernel; CONV_GEMM for
@@ -141,6 +144,18 @@ struct Net {
     // YH_CONV=<kernel id>
     std::map<GraphKey, std::vector<int>> conv_kern;
     const std::vector<int>* cur_kern = nullptr;
+    int force_kern = -1;   // yh_force_conv_kernel (testing); -1 = autotune / YH_CONV
+    // launch units of the forward at the current shape: a single op, or a run of
+    // ops fused into one level-program launch (csrc/level.hip)
+    struct Unit { int first, last; bool level; int lop_off, lop_cnt; };
+    struct Plan { std::vector<Unit> units; LevelOp* lops_dev = nullptr; int NC = 0, G = 0; std::vector<int> lds; };
+    std::map<GraphKey, Plan> plans;
+    const Plan* cur_plan = nullptr;
+    // level programs are opt-in (YH_LEVEL=1 or yh_set_level_fusion) until they beat
+    // the per-layer kernels
+    bool use_level = [] { const char* e = getenv("YH_LEVEL"); return e && atoi(e) != 0; }();
+    unsigned* bar_dev = nullptr;   // [32][64] cluster barrier words
+    int* lerr_dev = nullptr;       // level-program barrier timeout flag
 
     // ---------------------------------------------------------- builder
     int tensor(int level, int C) {
@@ -207,14 +222,19 @@ struct Net {
         conv3(p + ".conv2", full(t), hid, ch, 1, ACT_SILU, out, &x);
     }
     // CSPModule / C3k (nn.py:52-63)
+    // The residual chain a -> a' -> a'' runs through fresh tensors (not in place)
+    // so that no region is rewritten after a 3x3 conv of another workgroup read
+    // it (the level program's hand-off rule, csrc/level.hip); the last link
+    // writes into the concat buffer.
     void cspmodule(const std::string& p, View x, int in_ch, int out_ch, View out, int level) {
         const int h = out_ch / 2;
         const int t = tensor(level, 2 * h);
         View a = slice(t, 0, h), b = slice(t, h, h);
-        conv1(p + ".conv1", x, in_ch, h, ACT_SILU, a);
+        const int a0 = tensor(level, h), a1 = tensor(level, h);
+        conv1(p + ".conv1", x, in_ch, h, ACT_SILU, full(a0));
         conv1(p + ".conv2", x, in_ch, h, ACT_SILU, b);
-        residual(p + ".res_m.0", a, h, 1.0, a, level);
-        residual(p + ".res_m.1", a, h, 1.0, a, level);
+        residual(p + ".res_m.0", full(a0), h, 1.0, full(a1), level);
+        residual(p + ".res_m.1", full(a1), h, 1.0, a, level);
         conv1(p + ".conv3", full(t), 2 * h, out_ch, ACT_SILU, out);
     }
     // CSP / C3k2 (nn.py:66-80); input may be a 2-segment (optionally upsampled) concat
@@ -331,17 +351,16 @@ struct Net {
         const int xs[3] = {P3, P4, P5};
         const int xc[3] = {w[3], w[4], w[5]};
         int L[3];
-        for (int l = 0; l < 3; ++l) {
+        // per level, coarsest first: the 20x20 and 40x40 head branches join the
+        // level program that computes P5 / P4; the 80x80 level runs last
+        for (int l = 0; l < 3; ++l) L[l] = tensor(3 + l, 64 + ncp);
+        for (int l : {2, 1, 0}) {
             const int lvl = 3 + l;
-            L[l] = tensor(lvl, 64 + ncp);
             const std::string bp = "head.box." + std::to_string(l);
             const int tb1 = tensor(lvl, boxc), tb2 = tensor(lvl, boxc);
             conv3(bp + ".0", full(xs[l], xc[l]), xc[l], boxc, 1, ACT_SILU, full(tb1, boxc));
             conv3(bp + ".1", full(tb1, boxc), boxc, boxc, 1, ACT_SILU, full(tb2, boxc));
             dense(bp + ".2", {Seg{full(tb2, boxc), 0}}, {boxc}, 64, 1, 1, ACT_ID, slice(L[l], 0, 64), nullptr, 1);
-        }
-        for (int l = 0; l < 3; ++l) {
-            const int lvl = 3 + l;
             const std::string cp = "head.cls." + std::to_string(l);
             const int tc1 = tensor(lvl, xc[l]), tc2 = tensor(lvl, clsc), tc3 = tensor(lvl, clsc), tc4 = tensor(lvl, clsc);
             dw(cp + ".0", full(xs[l], xc[l]), xc[l], full(tc1, xc[l]));
@@ -487,16 +506,24 @@ struct Net {
     }
 
     // ---------------------------------------------------------- workspace
+    // Tensors are laid out coarsest level first, so the 40x40 / 20x20 tensors and
+    // the 80x80 inputs of the level program sit in the first bytes of the
+    // workspace (it addresses them by 32-bit offsets).
     size_t ws_bytes_for(int B, int H, int W, std::vector<size_t>* offs) const {
         size_t total = 0;
         if (offs) offs->assign(tensors.size(), 0);
-        for (size_t i = 0; i < tensors.size(); ++i) {
-            const Tensor& t = tensors[i];
-            const size_t b = (size_t)B * (H >> t.level) * (W >> t.level) * t.C * es;
-            if (offs) (*offs)[i] = total;
-            total += (b + 255) & ~(size_t)255;
-        }
+        for (int lvl = 5; lvl >= 0; --lvl)
+            for (size_t i = 0; i < tensors.size(); ++i) {
+                const Tensor& t = tensors[i];
+                if (t.level != lvl) continue;
+                const size_t b = (size_t)B * (H >> t.level) * (W >> t.level) * t.C * es;
+                if (offs) (*offs)[i] = total;
+                total += (b + 255) & ~(size_t)255;
+            }
         return total;
+    }
+    size_t tensor_end(int t) const {
+        return ws.off[t] + (size_t)ws.B * (ws.H >> tensors[t].level) * (ws.W >> tensors[t].level) * tensors[t].C * es;
     }
     void reserve(int B, int H, int W) {
         require(B > 0 && H > 0 && W > 0 && H % 32 == 0 && W % 32 == 0, "input height/width must be positive multiples of 32");
@@ -526,6 +553,7 @@ struct Net {
     void drop_graphs() {
         for (auto& kv : graphs) (void)hipGraphExecDestroy(kv.second);
         graphs.clear();
+        free_plans();
     }
 
     // ---------------------------------------------------------- launches
@@ -566,6 +594,35 @@ struct Net {
         a.zero = zero_dev;
     }
 
+    DwArgs dw_args(const Op& op, int B, int H, int W) const {
+        const ConvDesc& d = convs[op.conv];
+        const Tensor& ti = tensors[op.in[0].v.t];
+        DwArgs a{};
+        a.in = ptr(op.in[0].v); a.ldi = ti.C;
+        a.H = H >> ti.level; a.W = W >> ti.level; a.C = d.cout_p; a.M = B * a.H * a.W;
+        a.w = (const float*)d.w_dev; a.bias = d.b_dev;
+        a.out = ptr(op.out); a.ldo = ldc(op.out); a.act = d.act;
+        return a;
+    }
+    PoolArgs pool_args(const Op& op, int B, int H, int W) const {
+        const Tensor& t = tensors[op.out.t];
+        PoolArgs a{};
+        a.buf = ptr(op.out); a.ldc = t.C; a.C = op.out.C; a.H = H >> t.level; a.W = W >> t.level; a.B = B;
+        return a;
+    }
+    AttnArgs attn_args(const Op& op, int H, int W) const {
+        const ConvDesc& d = convs[op.conv];
+        const Tensor& tq = tensors[op.in[0].v.t];
+        AttnArgs a{};
+        a.qkv = ptr(op.in[0].v); a.ldq = tq.C;
+        a.Hs = H >> tq.level; a.Ws = W >> tq.level; a.T = a.Hs * a.Ws;
+        a.heads = op.heads; a.dk = 32; a.dh = 64;
+        a.scale = (float)std::pow(32.0, -0.5);
+        a.pe_w = (const float*)d.w_dev; a.pe_b = d.b_dev;
+        a.out = ptr(op.out); a.ldo = ldc(op.out);
+        return a;
+    }
+
     // Pick the dense-conv kernel of every conv op for this shape: one plain forward
     // (realistic activations in the workspace), then each candidate kernel of each
     // conv timed over 3 launches after a warm-up launch. The candidates produce
@@ -576,7 +633,9 @@ struct Net {
         auto it = conv_kern.find(key);
         if (it != conv_kern.end()) { cur_kern = &it->second; return; }
         std::vector<int> ch(ops.size(), CONV_GEMM);
-        static const int forced = [] { const char* e = getenv("YH_CONV"); return e ? atoi(e) : -1; }();
+        static const int env_forced = [] { const char* e = getenv("YH_CONV"); return e ? atoi(e) : -1; }();
+        const int forced = force_kern >= 0 ? force_kern : env_forced;
+        static const bool tune_log = getenv("YH_TUNE_LOG") != nullptr;
         if (dtype != F32) {
             cur_kern = nullptr;
             std::vector<ConvArgs> args(ops.size());
@@ -591,8 +650,12 @@ struct Net {
                 hipEvent_t e0, e1;
                 HIPCHECK(hipEventCreate(&e0));
                 HIPCHECK(hipEventCreate(&e1));
+                std::vector<char> fused(ops.size(), 0);
+                if (cur_plan)
+                    for (auto& u : cur_plan->units)
+                        if (u.level) for (int k = u.first; k < u.last; ++k) fused[k] = 1;
                 for (size_t i = 0; i < ops.size(); ++i) {
-                    if (ops[i].kind != OP_CONV) continue;
+                    if (ops[i].kind != OP_CONV || fused[i]) continue;
                     float best = 1e30f;
                     for (int k = 0; k < CONV_NKERNELS; ++k) {
                         if (!conv_kernel_ok(dtype, k, args[i])) continue;
@@ -604,6 +667,7 @@ struct Net {
                         if (rc != 0) throw Fail(YH_EHIP, "tuning launch of " + ops[i].label + " failed");
                         float ms = 0.f;
                         HIPCHECK(hipEventElapsedTime(&ms, e0, e1));
+                        if (tune_log) fprintf(stderr, "[yh tune] %-36s kernel %d  %8.2f us\n", ops[i].label.c_str(), k, ms * 1e3f / 3);
                         if (ms < best) { best = ms; ch[i] = k; }
                     }
                 }
@@ -641,37 +705,9 @@ struct Net {
                 rc = launch_conv(dtype, kern, BM, BN, a, s);
                 break;
             }
-            case OP_DW: {
-                const ConvDesc& d = convs[op.conv];
-                const Tensor& ti = tensors[op.in[0].v.t];
-                DwArgs a{};
-                a.in = ptr(op.in[0].v); a.ldi = ti.C;
-                a.H = H >> ti.level; a.W = W >> ti.level; a.C = d.cout_p; a.M = B * a.H * a.W;
-                a.w = (const float*)d.w_dev; a.bias = d.b_dev;
-                a.out = ptr(op.out); a.ldo = ldc(op.out); a.act = d.act;
-                rc = launch_dwconv(dtype, a, s);
-                break;
-            }
-            case OP_SPPF: {
-                const Tensor& t = tensors[op.out.t];
-                PoolArgs a{};
-                a.buf = ptr(op.out); a.ldc = t.C; a.C = op.out.C; a.H = H >> t.level; a.W = W >> t.level; a.B = B;
-                rc = launch_sppf(dtype, a, s);
-                break;
-            }
-            case OP_ATTN: {
-                const ConvDesc& d = convs[op.conv];
-                const Tensor& tq = tensors[op.in[0].v.t];
-                AttnArgs a{};
-                a.qkv = ptr(op.in[0].v); a.ldq = tq.C;
-                a.Hs = H >> tq.level; a.Ws = W >> tq.level; a.T = a.Hs * a.Ws;
-                a.heads = op.heads; a.dk = 32; a.dh = 64;
-                a.scale = (float)std::pow(32.0, -0.5);
-                a.pe_w = (const float*)d.w_dev; a.pe_b = d.b_dev;
-                a.out = ptr(op.out); a.ldo = ldc(op.out);
-                rc = launch_attention(dtype, a, B, s);
-                break;
-            }
+            case OP_DW: rc = launch_dwconv(dtype, dw_args(op, B, H, W), s); break;
+            case OP_SPPF: rc = launch_sppf(dtype, pool_args(op, B, H, W), s); break;
+            case OP_ATTN: rc = launch_attention(dtype, attn_args(op, H, W), B, s); break;
             case OP_DECODE: {
                 DecodeArgs a{};
                 for (int l = 0; l < 3; ++l) {
@@ -692,8 +728,352 @@ struct Net {
         if (rc != 0) throw Fail(YH_EHIP, "launch of " + op.label + " failed: " + hipGetErrorString((hipError_t)rc));
     }
 
+    // ---------------------------------------------------------- level program
+    int out_level(const Op& op) const {
+        if (op.kind == OP_DECODE) return 0;
+        return tensors[op.out.t].level;
+    }
+    bool level_eligible(const Op& op) const {
+        if (dtype == F32 || !use_level) return false;
+        if (op.kind == OP_FIRST || op.kind == OP_DECODE) return false;
+        if (out_level(op) < 4) return false;
+        if (op.kind == OP_CONV && convs[op.conv].Kp / 8 > level_ktab_max()) return false;
+        return true;
+    }
+    // Reads that cross the pixel partition of the op's level (halo, stride,
+    // upsample, attention keys, pools) versus pixel-local ones (1x1 at the
+    // same level, residuals, depthwise centre excluded).
+    bool pixel_local(const Op& op) const {
+        if (op.kind != OP_CONV) return false;
+        const ConvDesc& d = convs[op.conv];
+        if (d.k != 1 || d.stride != 1) return false;
+        for (auto& sg : op.in)
+            if (sg.up || tensors[sg.v.t].level != tensors[op.out.t].level) return false;
+        return true;
+    }
+    // Hand-off rule of the level program: within one launch, no channel range of a
+    // tensor is written after a non-pixel-local read of it, and pixel-local
+    // in-place rewrites only touch tensors whose pixel rows fill whole 128-B lines.
+    bool segment_safe(int first, int last) const {
+        struct Rng { int t, c0, c1; };
+        std::vector<Rng> nonlocal, written;
+        auto overlap = [](const Rng& a, const Rng& b) { return a.t == b.t && a.c0 < b.c1 && b.c0 < a.c1; };
+        for (int i = first; i < last; ++i) {
+            const Op& op = ops[i];
+            std::vector<Rng> reads;
+            for (auto& sg : op.in) reads.push_back({sg.v.t, sg.v.coff, sg.v.coff + sg.v.C});
+            if (op.res.t >= 0 && op.has_res) reads.push_back({op.res.t, op.res.coff, op.res.coff + op.res.C});
+            const bool local = pixel_local(op);
+            std::vector<Rng> outs;
+            if (op.kind == OP_SPPF) {
+                // pool i reads slice i, writes slice i+1: writes never precede a read of themselves
+                const int C = op.out.C;
+                for (int k = 0; k < 3; ++k) {
+                    const Rng w{op.out.t, op.out.coff + (k + 1) * C, op.out.coff + (k + 2) * C};
+                    for (auto& r : nonlocal)
+                        if (overlap(w, r)) return false;
+                    nonlocal.push_back({op.out.t, op.out.coff + k * C, op.out.coff + (k + 1) * C});
+                    written.push_back(w);
+                }
+                continue;
+            }
+            for (auto& r : reads)
+                if (!local) nonlocal.push_back(r);
+            outs.push_back({op.out.t, op.out.coff, op.out.coff + op.out.C});
+            for (auto& w : outs) {
+                for (auto& r : nonlocal)
+                    if (overlap(w, r)) return false;
+                for (auto& r : written)
+                    if (overlap(w, r) && (tensors[w.t].C * es) % 128 != 0) return false;
+                written.push_back(w);
+            }
+        }
+        return true;
+    }
+    // LDS bytes of the largest input patch (rows of the workgroup's output pixels
+    // plus the conv's halo, zero border, all input channels) over the G members
+    static constexpr int LEVEL_PATCH_MAX = 112 * 1024;
+    // worst-case LDS bytes of a band of `tiles` 16-pixel tiles (any alignment)
+    static int band_bytes(const ConvArgs& c, int tiles) {
+        const int rows_out = (16 * tiles - 1 + c.Wo - 1) / c.Wo + 1;
+        const int rows_in = (rows_out - 1) * c.stride + c.KH;
+        return rows_in * (c.Wi + 2 * c.pad) * (c.Cin * 2 + 16) + 16;
+    }
+    // largest band (in tiles, <= a member's tile count) within the LDS budget; 0 = none fits
+    static int patch_band(const ConvArgs& c, int G) {
+        const int npt = (c.Ho * c.Wo + 15) / 16;
+        const int per = (npt + G - 1) / G;
+        int b = 0;
+        while (b < per && band_bytes(c, b + 1) <= LEVEL_PATCH_MAX) ++b;
+        return b;
+    }
+    static int patch_bytes(const ConvArgs& c, int band) { return band > 0 ? band_bytes(c, band) : 0; }
+    int G_ = 8;   // cluster size of the plan being built
+    static constexpr int LEVEL_LDS_MAX = 136 * 1024;   // dynamic LDS of the level program
+    static constexpr int LEVEL_WBUF_MAX = 64 * 1024;   // both weight chunk buffers together
+    // Patch conv plan: cout chunk width nt, wave grid wn x (8 / wn), weight chunk
+    // depth kcs, band size (one block of <= 4 pixel tiles per wave and band) and the
+    // LDS layout [zero fragment | patch | weight chunk x 2]. patch = 0 if nothing fits.
+    void plan_patch_conv(LevelOp& L) const {
+        // Candidates: cout chunk width nt, cluster split pc (cout ranges) x G/pc (pixel
+        // ranges). Each is costed in memory round trips per workgroup (one per patch
+        // band, one per weight chunk of every band; ~1.4 us each under load) plus
+        // MFMA time; the cheapest that fits the LDS budget wins.
+        const ConvArgs& c = L.c;
+        const int nct = (c.Cout + 15) / 16;
+        const int nks = (c.K + 31) / 32;
+        const int npt = (c.Ho * c.Wo + 15) / 16;
+        double best = 1e30;
+        LevelOp bestL = L;
+        bestL.patch = 0;
+        for (int nt : {4, 2, 1}) {
+            if (nt > 1 && nct < nt) continue;
+            const int nchall = (nct + nt - 1) / nt;
+            for (int pc : {1, 2, 4, 8}) {
+                if (pc > G_ || G_ % pc || pc > nchall) continue;
+                const int nch = (nchall + pc - 1) / pc;           // chunks of the largest range
+                const int wn = nch >= 8 ? 8 : nch >= 4 ? 4 : nch >= 2 ? 2 : 1;
+                if (nch > wn) continue;                           // one cout chunk per wave column
+                const int wm = 8 / wn;
+                const int wrows = nch * 16 * nt;
+                int kcs = 1;
+                while (kcs < nks && 2 * wrows * ((kcs + 1) * 64 + 16) <= LEVEL_WBUF_MAX && wrows * (kcs + 1) * 4 <= 8 * 512)
+                    ++kcs;
+                if (2 * wrows * (kcs * 64 + 16) > LEVEL_WBUF_MAX || wrows * kcs * 4 > 8 * 512) continue;
+                const int wbytes = 2 * wrows * (kcs * 64 + 16);
+                const int pm = G_ / pc;
+                const int tiles = (npt + pm - 1) / pm;
+                int band = 0;
+                while (band < std::min(tiles, wm * 4) && band_bytes(c, band + 1) + wbytes <= LEVEL_LDS_MAX) ++band;
+                if (band == 0) continue;
+                const int bands = (tiles + band - 1) / band;
+                const int chunks = (nks + kcs - 1) / kcs;
+                const double mfma_us = (double)tiles * nch * nt * nks * 16 / 4 / 2.1e3;   // 4 SIMDs, ~2.1 GHz
+                const double cost = bands * (1 + chunks) * 1.4 + mfma_us;
+                if (cost < best - 1e-9) {
+                    best = cost;
+                    bestL = L;
+                    bestL.nt = nt; bestL.pc = pc; bestL.wn = wn; bestL.kcs = kcs; bestL.wpitch = kcs * 64 + 16;
+                    bestL.band = band; bestL.woff = (band_bytes(c, band) + 15) / 16 * 16; bestL.patch = 1;
+                }
+            }
+        }
+        L = bestL;
+        if (!L.patch) {
+            L.nt = nct >= 4 ? 4 : nct >= 2 ? 2 : 1;
+            L.pc = 1;
+        }
+    }
+    LevelOp level_op(const Op& op, int B, int H, int W, int sub) const {
+        LevelOp L;
+        std::memset(&L, 0, sizeof(L));
+        switch (op.kind) {
+            case OP_CONV: {
+                int BM, BN;
+                L.kind = LOP_CONV;
+                conv_args(op, B, H, W, L.c, BM, BN);
+                const int nct = (L.c.Cout + 15) / 16;
+                L.nt = nct >= 4 ? 4 : nct >= 2 ? 2 : 1;
+                L.pstride = L.c.Cin * 2 + 16;
+                L.wp = L.c.Wi + 2 * L.c.pad;
+                L.wcount = convs[op.conv].coutp_pad * convs[op.conv].Kp;
+                L.bcount = convs[op.conv].coutp_pad;
+                plan_patch_conv(L);
+                break;
+            }
+            case OP_DW: L.kind = LOP_DW; L.d = dw_args(op, B, H, W); break;
+            case OP_SPPF: L.kind = LOP_POOL; L.step = sub; L.pl = pool_args(op, B, H, W); break;
+            case OP_ATTN: L.kind = LOP_ATTN; L.at = attn_args(op, H, W); break;
+            default: throw Fail(YH_EINVAL, "op kind not supported by the level program");
+        }
+        return L;
+    }
+    // Which level ops need the cluster barrier before them: those reading data
+    // written since the last barrier other than their own pixels at their own
+    // level (3x3 / strided / upsampled / attention / pool / depthwise reads, or a
+    // 1x1 reading another level's partition). SPPF is three pool ops, each
+    // reading the previous one's output.
+    // A pixel-local read of data written since the last barrier is safe only if
+    // writer and reader split the image's pixels the same way (the G-way pixel
+    // partition: convs with pc == 1, depthwise, pools) at the same level.
+    // Host replay of the patch conv's index arithmetic for every member of a
+    // cluster: weight / bias / k-table reads inside their allocations, the patch
+    // and both weight buffers inside the planned LDS. Throws on a planning bug.
+    void validate_level_op(const LevelOp& L, int G) const {
+        if (L.kind != LOP_CONV || !L.patch) return;
+        const ConvArgs& c = L.c;
+        const int P = c.Ho * c.Wo, npt = (P + 15) / 16;
+        const int nchall = (c.Cout + 16 * L.nt - 1) / (16 * L.nt);
+        const int pm = G / L.pc;
+        require(G % L.pc == 0 && L.pc >= 1, "level op: bad cluster split");
+        require(c.Kp / 8 <= level_ktab_max(), "level op: k-table too long");
+        const int wrows_plan = (nchall + L.pc - 1) / L.pc * 16 * L.nt;
+        const long long wcount = (long long)L.wcount;
+        for (int m = 0; m < G; ++m) {
+            const int mp = m / L.pc, mc = m % L.pc;
+            const int ch0 = mc * nchall / L.pc, ch1 = (mc + 1) * nchall / L.pc;
+            const int p0 = mp * npt / pm * 16, p1 = std::min(P, (mp + 1) * npt / pm * 16);
+            if (p1 <= p0 || ch1 <= ch0) continue;
+            const int wrows = (ch1 - ch0) * 16 * L.nt;
+            require(wrows <= wrows_plan, "level op: weight rows exceed plan");
+            require(wrows * L.kcs * 4 <= 8 * 512, "level op: weight chunk exceeds staging registers");
+            const long long max_cout = (long long)ch1 * 16 * L.nt - 1;
+            require((max_cout + 1) * c.Kp <= wcount, "level op: weight rows outside the packed weights");
+            require(ch1 * 16 * L.nt <= L.bcount + 16, "level op: bias outside allocation");
+            for (int q0 = p0; q0 < p1; q0 += 16 * L.band) {
+                const int q1 = std::min(p1, q0 + 16 * L.band);
+                const int ho0 = q0 / c.Wo, ho1 = (q1 - 1) / c.Wo;
+                const int nrows = (ho1 - ho0) * c.stride + c.KH;
+                const long long patch_end = 16 + (long long)nrows * L.wp * L.pstride;
+                require(patch_end <= L.woff, "level op: patch overlaps the weight buffers");
+                // largest fragment read: last pixel, largest k offset
+                const int pc = q1 - 1, ho = pc / c.Wo, wo = pc - ho * c.Wo;
+                const long long lb = 16 + ((long long)(ho - ho0) * c.stride * L.wp + (long long)wo * c.stride) * L.pstride;
+                const long long kmax_off = ((long long)(c.KH - 1) * L.wp + (c.KW - 1)) * L.pstride + (c.Cin - 8) * 2;
+                require(lb + kmax_off + 16 <= patch_end, "level op: fragment read outside the patch");
+            }
+        }
+    }
+
+    void mark_syncs(int first, int last, LevelOp* lo) const {
+        struct Rng { int t, c0, c1, level; bool gpart; };
+        std::vector<Rng> w;
+        auto hit = [&](int t, int c0, int c1, bool local, int lvl) {
+            for (auto& r : w)
+                if (r.t == t && r.c0 < c1 && c0 < r.c1 && (!local || r.level != lvl || !r.gpart)) return true;
+            return false;
+        };
+        int k = 0;
+        for (int i = first; i < last; ++i) {
+            const Op& op = ops[i];
+            const int lvl = tensors[op.out.t].level;
+            if (op.kind == OP_SPPF) {
+                for (int sub = 0; sub < 3; ++sub, ++k) {
+                    const int c0 = op.out.coff + sub * op.out.C;
+                    lo[k].sync = (k == 0 || hit(op.out.t, c0, c0 + op.out.C, false, lvl)) ? 1 : 0;
+                    if (lo[k].sync) w.clear();
+                    if (k == 0) lo[k].sync = 0;
+                    w.push_back({op.out.t, c0 + op.out.C, c0 + 2 * op.out.C, lvl, true});
+                }
+                continue;
+            }
+            const bool gpart = op.kind == OP_DW || (op.kind == OP_CONV && (lo[k].kind != LOP_CONV || !lo[k].patch || lo[k].pc == 1));
+            const bool local = pixel_local(op) && gpart;
+            bool need = false;
+            for (auto& sg : op.in) need |= hit(sg.v.t, sg.v.coff, sg.v.coff + sg.v.C, local, lvl);
+            if (op.has_res) need |= hit(op.res.t, op.res.coff, op.res.coff + op.res.C, true, lvl);
+            lo[k].sync = (k > 0 && need) ? 1 : 0;
+            if (lo[k].sync) w.clear();
+            w.push_back({op.out.t, op.out.coff, op.out.coff + op.out.C, lvl, gpart});
+            ++k;
+        }
+    }
+    void free_plans() {
+        for (auto& kv : plans)
+            if (kv.second.lops_dev) (void)hipFree(kv.second.lops_dev);
+        plans.clear();
+        cur_plan = nullptr;
+    }
+    void ensure_plan(int B, int H, int W) {
+        const GraphKey key{B, H, W};
+        auto it = plans.find(key);
+        if (it != plans.end()) { cur_plan = &it->second; return; }
+        Plan pl;
+        pl.NC = std::min(32, (B + 7) / 8 * 8);
+        pl.G = 256 / pl.NC;
+        G_ = pl.G;
+        std::vector<LevelOp> lops;
+        size_t i = 0;
+        while (i < ops.size()) {
+            size_t j = i;
+            while (j < ops.size() && level_eligible(ops[j])) ++j;
+            bool fuse = j - i >= 2 && segment_safe((int)i, (int)j);
+            if (fuse) {   // every tensor the run touches must be addressable by a 31-bit offset
+                for (size_t k = i; k < j && fuse; ++k) {
+                    std::vector<int> ts{ops[k].out.t};
+                    for (auto& sg : ops[k].in) ts.push_back(sg.v.t);
+                    if (ops[k].has_res) ts.push_back(ops[k].res.t);
+                    for (int t : ts)
+                        if (tensor_end(t) >= ((size_t)1 << 31) - 4096) fuse = false;
+                }
+            }
+            if (fuse) {
+                Unit u{(int)i, (int)j, true, (int)lops.size(), 0};
+                for (size_t k = i; k < j; ++k) {
+                    const int subs = ops[k].kind == OP_SPPF ? 3 : 1;
+                    for (int sub = 0; sub < subs; ++sub) lops.push_back(level_op(ops[k], B, H, W, sub));
+                }
+                u.lop_cnt = (int)lops.size() - u.lop_off;
+                mark_syncs((int)i, (int)j, lops.data() + u.lop_off);
+                for (int k = u.lop_off; k < (int)lops.size(); ++k) validate_level_op(lops[k], pl.G);
+                int lds = 0;
+                for (int k = u.lop_off; k < (int)lops.size(); ++k)
+                    if (lops[k].kind == LOP_CONV && lops[k].patch) {
+                        const int nchall = (lops[k].c.Cout + 16 * lops[k].nt - 1) / (16 * lops[k].nt);
+                        const int wrows = (nchall + lops[k].pc - 1) / lops[k].pc * 16 * lops[k].nt;
+                        lds = std::max(lds, lops[k].woff + 2 * wrows * lops[k].wpitch);
+                    }
+                pl.lds.push_back(lds);
+                pl.units.push_back(u);
+                i = j;
+            } else {
+                pl.units.push_back(Unit{(int)i, (int)i + 1, false, 0, 0});
+                pl.lds.push_back(0);
+                ++i;
+            }
+        }
+        if (!lops.empty()) {
+            HIPCHECK(hipMalloc(&pl.lops_dev, lops.size() * sizeof(LevelOp)));
+            HIPCHECK(hipMemcpy(pl.lops_dev, lops.data(), lops.size() * sizeof(LevelOp), hipMemcpyHostToDevice));
+            if (!bar_dev) {
+                HIPCHECK(hipMalloc(&bar_dev, 32 * 64 * sizeof(unsigned)));
+                HIPCHECK(hipMemset(bar_dev, 0, 32 * 64 * sizeof(unsigned)));
+                HIPCHECK(hipMalloc(&lerr_dev, sizeof(int)));
+                HIPCHECK(hipMemset(lerr_dev, 0, sizeof(int)));
+            }
+        }
+        cur_plan = &plans.emplace(key, std::move(pl)).first->second;
+    }
+    void launch_unit(const Unit& u, int B, int H, int W, hipStream_t s) {
+        launch_unit_(u, B, H, W, s);
+        // YH_SYNC_UNITS=1 (debugging): synchronize after every launch unit outside graph
+        // capture, so a device fault is reported with the unit that caused it
+        static const bool sync_units = getenv("YH_SYNC_UNITS") != nullptr;
+        if (sync_units) {
+            hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+            (void)hipStreamIsCapturing(s, &st);
+            if (st == hipStreamCaptureStatusNone) {
+                const hipError_t e = hipStreamSynchronize(s);
+                if (e != hipSuccess)
+                    throw Fail(YH_EHIP, "unit " + ops[u.first].label + (u.level ? " (level program)" : "") + ": " +
+                                            hipGetErrorString(e));
+            }
+        }
+    }
+    void launch_unit_(const Unit& u, int B, int H, int W, hipStream_t s) {
+        if (!u.level) { launch_op(u.first, B, H, W, s); return; }
+        LevelArgs a{};
+        a.ops = cur_plan->lops_dev + u.lop_off;
+        a.nops = u.lop_cnt;
+        a.B = B; a.G = cur_plan->G; a.NC = cur_plan->NC;
+        a.base = ws.base;
+        a.bar = bar_dev;
+        a.err = lerr_dev;
+        a.lds_patch = cur_plan->lds[&u - cur_plan->units.data()];
+        static const int skip = [] { const char* e = getenv("YH_LEVEL_SKIP"); return e ? atoi(e) : 0; }();
+        a.skip = skip;
+        a.trace = level_trace_ptr ? level_trace_ptr + 8 * u.lop_off : nullptr;
+        const int rc = launch_level(dtype, a, s);
+        if (rc != 0) throw Fail(YH_EHIP, "level program launch (" + ops[u.first].label + " .. " + ops[u.last - 1].label +
+                                         ") failed: " + hipGetErrorString((hipError_t)rc));
+    }
+
     void run_ops(int B, int H, int W, hipStream_t s) {
-        for (size_t i = 0; i < ops.size(); ++i) launch_op(i, B, H, W, s);
+        if (!cur_plan) {
+            for (size_t i = 0; i < ops.size(); ++i) launch_op(i, B, H, W, s);
+            return;
+        }
+        for (auto& u : cur_plan->units) launch_unit(u, B, H, W, s);
     }
 
     void forward(const void* x, int B, int H, int W, void* y, hipStream_t s) {
@@ -701,23 +1081,28 @@ struct Net {
         reserve(B, H, W);
         HIPCHECK(hipSetDevice(device));
         require(launch_set_io(io_dev, x, y, s) == 0, "set_io launch failed", YH_EHIP);
+        ensure_plan(B, H, W);
         ensure_tuned(B, H, W, s);
         lastB = B; lastH = H; lastW = W;
-        if (profile) {
-            if (ev.size() < 2 * ops.size()) {
+        if (profile) {   // HIP events around every launch unit, on the caller's stream
+            const size_t nu = cur_plan->units.size();
+            if (ev.size() < 2 * nu) {
                 for (auto e : ev) (void)hipEventDestroy(e);
-                ev.assign(2 * ops.size(), nullptr);
+                ev.assign(2 * nu, nullptr);
                 for (auto& e : ev) HIPCHECK(hipEventCreate(&e));
             }
-            prof_ms.resize(ops.size(), 0.0);
-            prof_calls.resize(ops.size(), 0);
-            for (size_t i = 0; i < ops.size(); ++i) {
+            if (prof_key.B != B || prof_key.H != H || prof_key.W != W) {
+                prof_ms.assign(nu, 0.0);
+                prof_calls.assign(nu, 0);
+                prof_key = GraphKey{B, H, W};
+            }
+            for (size_t i = 0; i < nu; ++i) {
                 HIPCHECK(hipEventRecord(ev[2 * i], s));
-                launch_op(i, B, H, W, s);
+                launch_unit(cur_plan->units[i], B, H, W, s);
                 HIPCHECK(hipEventRecord(ev[2 * i + 1], s));
             }
-            HIPCHECK(hipEventSynchronize(ev[2 * ops.size() - 1]));
-            for (size_t i = 0; i < ops.size(); ++i) {
+            HIPCHECK(hipEventSynchronize(ev[2 * nu - 1]));
+            for (size_t i = 0; i < nu; ++i) {
                 float ms = 0.f;
                 HIPCHECK(hipEventElapsedTime(&ms, ev[2 * i], ev[2 * i + 1]));
                 prof_ms[i] += ms;
@@ -823,6 +1208,9 @@ struct Net {
 
     ~Net() {
         drop_graphs();
+        free_plans();
+        if (bar_dev) (void)hipFree(bar_dev);
+        if (lerr_dev) (void)hipFree(lerr_dev);
         for (auto& d : convs) free_conv(d);
         if (ws.base) (void)hipFree(ws.base);
         if (io_dev) (void)hipFree(io_dev);
@@ -923,6 +1311,7 @@ int yh_load_conv(yh_handle* h, int index, const float* weight, const float* bias
         yh::require(!bn_gamma || (bn_beta && bn_mean && bn_var), "BatchNorm needs gamma, beta, mean and var");
         HIPCHECK(hipSetDevice(h->net.device));
         h->net.load_conv(index, weight, bias, bn_gamma, bn_beta, bn_mean, bn_var, bn_eps);
+        h->net.drop_graphs();   // captured graphs and level programs hold the old weight pointers
     });
 }
 
@@ -964,6 +1353,18 @@ int yh_forward(yh_handle* h, const void* x, int batch, int height, int width, vo
 size_t yh_nms_workspace_bytes(int batch, int num_classes, int anchors) {
     if (batch <= 0 || num_classes <= 0 || anchors <= 0) return 0;
     return (size_t)batch * anchors * num_classes * 8 + (size_t)batch * 4 + (size_t)batch * 2048 * 4 + 512;
+}
+
+// Debug hook (not part of the ABI header): yh_debug_level_trace(buf) makes later
+// level-program launches record, for block 0, s_memrealtime (100 MHz) on arrival
+// at and departure from the barrier after every level op: buf[2*k], buf[2*k+1]
+// for level op k of the plan (ops of all level units, in order); nullptr = off.
+// Graphs captured before the call keep their old setting.
+extern "C" int yh_debug_level_op_label(const yh_handle* h, int batch, int height, int width, int k,
+                                       const char** label);
+extern "C" int yh_debug_level_trace(void* device_buf) {
+    level_trace_ptr = (unsigned long long*)device_buf;
+    return 0;
 }
 
 // Debug hook (not part of the ABI header): yh_debug_nms_trace(buf) makes later
@@ -1026,6 +1427,49 @@ int yh_nms(int dtype, const void* y, int batch, int num_classes, int anchors, fl
     });
 }
 
+int yh_unit_count(const yh_handle* h, int batch, int height, int width) {
+    if (!h) return YH_EINVAL;
+    auto it = h->net.plans.find(yh::GraphKey{batch, height, width});
+    if (it == h->net.plans.end()) return YH_ESTATE;
+    return (int)it->second.units.size();
+}
+
+int yh_unit_info(const yh_handle* h, int index, int batch, int height, int width, int* first_op, int* num_ops,
+                 int* is_level, double* ms_total, int* calls) {
+    return guarded([&] {
+        yh::require(h, "null handle");
+        const yh::Net& n = h->net;
+        auto it = n.plans.find(yh::GraphKey{batch, height, width});
+        yh::require(it != n.plans.end(), "no forward has run at this shape yet", YH_ESTATE);
+        const auto& us = it->second.units;
+        yh::require(index >= 0 && index < (int)us.size(), "unit index out of range");
+        const bool prof_here = n.prof_key.B == batch && n.prof_key.H == height && n.prof_key.W == width;
+        if (first_op) *first_op = us[index].first;
+        if (num_ops) *num_ops = us[index].last - us[index].first;
+        if (is_level) *is_level = us[index].level ? 1 : 0;
+        if (ms_total) *ms_total = prof_here && index < (int)n.prof_ms.size() ? n.prof_ms[index] : 0.0;
+        if (calls) *calls = prof_here && index < (int)n.prof_calls.size() ? n.prof_calls[index] : 0;
+    });
+}
+
+int yh_set_level_fusion(yh_handle* h, int enable) {
+    return guarded([&] {
+        yh::require(h, "null handle");
+        h->net.use_level = enable != 0;
+        h->net.drop_graphs();
+        h->net.conv_kern.clear();
+        h->net.cur_kern = nullptr;
+    });
+}
+
+int yh_level_status(const yh_handle* h) {
+    if (!h) return YH_EINVAL;
+    if (!h->net.lerr_dev) return 0;
+    int v = 0;
+    if (hipMemcpy(&v, h->net.lerr_dev, sizeof(int), hipMemcpyDeviceToHost) != hipSuccess) return YH_EHIP;
+    return v;
+}
+
 int yh_set_graph(yh_handle* h, int enable) {
     return guarded([&] {
         yh::require(h, "null handle");
@@ -1048,13 +1492,24 @@ int yh_profile_reset(yh_handle* h) {
     });
 }
 
+int yh_force_conv_kernel(yh_handle* h, int kernel) {
+    return guarded([&] {
+        yh::require(h, "null handle");
+        yh::require(kernel >= -1 && kernel < yh::CONV_NKERNELS, "conv kernel id out of range");
+        h->net.force_kern = kernel;
+        h->net.conv_kern.clear();
+        h->net.cur_kern = nullptr;
+        h->net.drop_graphs();
+    });
+}
+
 int yh_op_count(const yh_handle* h) { return h ? (int)h->net.ops.size() : YH_EINVAL; }
 
 int yh_op_kernel(const yh_handle* h, int index, int batch, int height, int width, const char** name) {
     return guarded([&] {
         yh::require(h && index >= 0 && index < (int)h->net.ops.size(), "op index out of range");
         const yh::Net& n = h->net;
-        static const char* conv_names[] = {"gemm", "gemm64", "gemm128", "stream", "direct"};
+        static const char* conv_names[] = {"gemm", "gemm64", "gemm128", "stream", "direct", "stream4", "stream8"};
         static const char* op_names[] = {"stem", "conv", "dwconv", "sppf", "attention", "decode"};
         const yh::Op& op = n.ops[index];
         if (op.kind != yh::OP_CONV) {
@@ -1083,8 +1538,37 @@ int yh_op_info(const yh_handle* h, int index, int batch, int height, int width, 
         n.op_cost(op, batch, height, width, b, f);
         if (bytes) *bytes = b;
         if (flops) *flops = f;
-        if (ms_total) *ms_total = index < (int)n.prof_ms.size() ? n.prof_ms[index] : 0.0;
-        if (calls) *calls = index < (int)n.prof_calls.size() ? n.prof_calls[index] : 0;
+        // profiled time of the op's own launch unit; 0 calls for ops fused into a level program
+        double ms = 0.0;
+        int nc = 0;
+        auto it = n.plans.find(yh::GraphKey{batch, height, width});
+        const bool prof_here = n.prof_key.B == batch && n.prof_key.H == height && n.prof_key.W == width;
+        if (it != n.plans.end() && prof_here) {
+            const auto& us = it->second.units;
+            for (size_t u = 0; u < us.size() && u < n.prof_ms.size(); ++u)
+                if (!us[u].level && us[u].first == index) { ms = n.prof_ms[u]; nc = n.prof_calls[u]; }
+        }
+        if (ms_total) *ms_total = ms;
+        if (calls) *calls = nc;
+    });
+}
+
+// Label of level op k of the plan at a shape (the op it belongs to; SPPF gives 3).
+int yh_debug_level_op_label(const yh_handle* h, int batch, int height, int width, int k, const char** label) {
+    return guarded([&] {
+        yh::require(h && label, "null argument");
+        auto it = h->net.plans.find(yh::GraphKey{batch, height, width});
+        yh::require(it != h->net.plans.end(), "no plan at this shape", YH_ESTATE);
+        for (auto& u : it->second.units) {
+            if (!u.level) continue;
+            int idx = u.lop_off;
+            for (int o = u.first; o < u.last; ++o) {
+                const int subs = h->net.ops[o].kind == yh::OP_SPPF ? 3 : 1;
+                for (int sub = 0; sub < subs; ++sub, ++idx)
+                    if (idx == k) { *label = h->net.ops[o].label.c_str(); return; }
+            }
+        }
+        yh::require(false, "level op index out of range");
     });
 }
 

@@ -50,6 +50,12 @@ _PROTOS = {
                            POINTER(c_double), POINTER(c_double), POINTER(c_double), POINTER(c_int)]),
     "yh_set_graph": (c_int, [c_void_p, c_int]),
     "yh_op_kernel": (c_int, [c_void_p, c_int, c_int, c_int, c_int, POINTER(c_char_p)]),
+    "yh_force_conv_kernel": (c_int, [c_void_p, c_int]),
+    "yh_unit_count": (c_int, [c_void_p, c_int, c_int, c_int]),
+    "yh_unit_info": (c_int, [c_void_p, c_int, c_int, c_int, c_int, POINTER(c_int), POINTER(c_int), POINTER(c_int),
+                             POINTER(c_double), POINTER(c_int)]),
+    "yh_set_level_fusion": (c_int, [c_void_p, c_int]),
+    "yh_level_status": (c_int, [c_void_p]),
 }
 
 _lib = None

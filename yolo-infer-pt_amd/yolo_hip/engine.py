@@ -146,6 +146,38 @@ class Engine:
     def set_graph(self, enable):
         check(lib().yh_set_graph(self._h, int(bool(enable))))
 
+    def force_conv_kernel(self, kernel):
+        """Run dense convs on one kernel implementation (0..6), or -1 for per-shape autotuning."""
+        check(lib().yh_force_conv_kernel(self._h, int(kernel)), "force_conv_kernel")
+
+    def set_level_fusion(self, enable):
+        """Fuse the 40x40 / 20x20 levels into level-program launches (default on, 16-bit only)."""
+        check(lib().yh_set_level_fusion(self._h, int(bool(enable))), "set_level_fusion")
+
+    def level_status(self):
+        """Raise if a level-program cluster barrier timed out (synchronizes the device)."""
+        rc = lib().yh_level_status(self._h)
+        if rc != 0:
+            raise RuntimeError(f"yolo_hip: level program barrier timeout / error ({rc})")
+
+    def units(self, batch, height, width):
+        """Launch units of the forward at this shape (after a forward), with profiled time."""
+        n = lib().yh_unit_count(self._h, int(batch), int(height), int(width))
+        if n < 0:
+            raise RuntimeError("yolo_hip: no forward has run at this shape yet")
+        ops = self.ops(batch, height, width)
+        out = []
+        for i in range(n):
+            f, k, lv, ms, calls = c_int(), c_int(), c_int(), c_double(), c_int()
+            check(lib().yh_unit_info(self._h, i, int(batch), int(height), int(width), byref(f), byref(k), byref(lv),
+                                     byref(ms), byref(calls)))
+            mem = ops[f.value:f.value + k.value]
+            out.append(dict(first=f.value, num_ops=k.value, level=bool(lv.value), ms=ms.value, calls=calls.value,
+                            label=mem[0]["label"] if k.value == 1 else f"level[{mem[0]['label']} .. {mem[-1]['label']}]",
+                            cls="level" if lv.value else mem[0]["cls"], kernel="level" if lv.value else mem[0]["kernel"],
+                            bytes=sum(o["bytes"] for o in mem), flops=sum(o["flops"] for o in mem), ops=mem))
+        return out
+
     def profile(self, enable):
         check(lib().yh_profile_enable(self._h, int(bool(enable))))
 
