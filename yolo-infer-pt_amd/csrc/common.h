@@ -125,11 +125,13 @@ struct LevelArgs {
     const LevelOp* ops; int nops;
     int B, G, NC;      // images, workgroups per cluster, clusters (grid = G * NC)
     const void* base;  // workspace base: activations are addressed by 32-bit byte offsets from it
-    unsigned* bar;     // [NC][64] barrier words (count at +0, generation at +32), zero-initialised
+    unsigned* bar;     // [NC][64] barrier words (count at +0, generation at +32), zero-initialised,
+                       // then [NC][32] XCC ids of the members
     int* err;          // set to 1 when a cluster barrier times out
     int lds_patch;     // dynamic LDS bytes for conv input patches
     int skip;          // debug: bit k set = skip ops of LevelOpKind k (timing experiments only)
-    unsigned long long* trace;  // debug: [nops][2] s_memrealtime of block 0 at each barrier (arrive, leave)
+    unsigned long long* trace;  // debug: [nops][8] s_memrealtime stamps of block 0 per op
+    int plain_ok;      // allow plain (L2-resident) activation stores in same-XCD clusters
 };
 int launch_level(int dtype, const LevelArgs& a, hipStream_t s);
 int level_ktab_max();

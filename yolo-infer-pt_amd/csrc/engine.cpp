@@ -735,6 +735,9 @@ struct Net {
     }
     bool level_eligible(const Op& op) const {
         if (dtype == F32 || !use_level) return false;
+        // clusters of 8 workgroups only (>= 25 images per launch): larger clusters
+        // (small batches) faulted on the device and are not yet understood
+        if (level_G_ != 8) return false;
         if (op.kind == OP_FIRST || op.kind == OP_DECODE) return false;
         if (out_level(op) < 4) return false;
         if (op.kind == OP_CONV && convs[op.conv].Kp / 8 > level_ktab_max()) return false;
@@ -809,7 +812,8 @@ struct Net {
     }
     static int patch_bytes(const ConvArgs& c, int band) { return band > 0 ? band_bytes(c, band) : 0; }
     int G_ = 8;   // cluster size of the plan being built
-    static constexpr int LEVEL_LDS_MAX = 136 * 1024;   // dynamic LDS of the level program
+    int level_G_ = 8;
+    static constexpr int LEVEL_LDS_MAX = 120 * 1024;   // dynamic LDS of the level program (static: ~24 KB)
     static constexpr int LEVEL_WBUF_MAX = 64 * 1024;   // both weight chunk buffers together
     // Patch conv plan: cout chunk width nt, wave grid wn x (8 / wn), weight chunk
     // depth kcs, band size (one block of <= 4 pixel tiles per wave and band) and the
@@ -844,7 +848,7 @@ struct Net {
                 const int pm = G_ / pc;
                 const int tiles = (npt + pm - 1) / pm;
                 int band = 0;
-                while (band < std::min(tiles, wm * 4) && band_bytes(c, band + 1) + wbytes <= LEVEL_LDS_MAX) ++band;
+                while (band < std::min(tiles, wm * 4) && band_bytes(c, band + 1) + 16 + wbytes <= LEVEL_LDS_MAX) ++band;
                 if (band == 0) continue;
                 const int bands = (tiles + band - 1) / band;
                 const int chunks = (nks + kcs - 1) / kcs;
@@ -982,6 +986,7 @@ struct Net {
         pl.NC = std::min(32, (B + 7) / 8 * 8);
         pl.G = 256 / pl.NC;
         G_ = pl.G;
+        level_G_ = pl.G;
         std::vector<LevelOp> lops;
         size_t i = 0;
         while (i < ops.size()) {
@@ -1006,6 +1011,19 @@ struct Net {
                 u.lop_cnt = (int)lops.size() - u.lop_off;
                 mark_syncs((int)i, (int)j, lops.data() + u.lop_off);
                 for (int k = u.lop_off; k < (int)lops.size(); ++k) validate_level_op(lops[k], pl.G);
+                static const bool dump = getenv("YH_LEVEL_DUMP") != nullptr;
+                if (dump) {
+                    int k = u.lop_off;
+                    for (size_t o = i; o < j; ++o) {
+                        const int subs = ops[o].kind == OP_SPPF ? 3 : 1;
+                        for (int sub = 0; sub < subs; ++sub, ++k) {
+                            const LevelOp& L = lops[k];
+                            fprintf(stderr, "[yh level] G=%d %-36s kind %d sync %d patch %d nt %d pc %d wn %d kcs %d band %d woff %d wpitch %d Cin %d Cout %d K %d Kp %d Ho %d Wo %d s %d\n",
+                                    pl.G, ops[o].label.c_str(), L.kind, L.sync, L.patch, L.nt, L.pc, L.wn, L.kcs, L.band, L.woff,
+                                    L.wpitch, L.c.Cin, L.c.Cout, L.c.K, L.c.Kp, L.c.Ho, L.c.Wo, L.c.stride);
+                        }
+                    }
+                }
                 int lds = 0;
                 for (int k = u.lop_off; k < (int)lops.size(); ++k)
                     if (lops[k].kind == LOP_CONV && lops[k].patch) {
@@ -1013,6 +1031,7 @@ struct Net {
                         const int wrows = (nchall + lops[k].pc - 1) / lops[k].pc * 16 * lops[k].nt;
                         lds = std::max(lds, lops[k].woff + 2 * wrows * lops[k].wpitch);
                     }
+                require(lds <= LEVEL_LDS_MAX, "level program LDS plan exceeds the budget");
                 pl.lds.push_back(lds);
                 pl.units.push_back(u);
                 i = j;
@@ -1026,8 +1045,8 @@ struct Net {
             HIPCHECK(hipMalloc(&pl.lops_dev, lops.size() * sizeof(LevelOp)));
             HIPCHECK(hipMemcpy(pl.lops_dev, lops.data(), lops.size() * sizeof(LevelOp), hipMemcpyHostToDevice));
             if (!bar_dev) {
-                HIPCHECK(hipMalloc(&bar_dev, 32 * 64 * sizeof(unsigned)));
-                HIPCHECK(hipMemset(bar_dev, 0, 32 * 64 * sizeof(unsigned)));
+                HIPCHECK(hipMalloc(&bar_dev, (32 * 64 + 32 * 32) * sizeof(unsigned)));
+                HIPCHECK(hipMemset(bar_dev, 0, (32 * 64 + 32 * 32) * sizeof(unsigned)));
                 HIPCHECK(hipMalloc(&lerr_dev, sizeof(int)));
                 HIPCHECK(hipMemset(lerr_dev, 0, sizeof(int)));
             }
@@ -1052,6 +1071,8 @@ struct Net {
     }
     void launch_unit_(const Unit& u, int B, int H, int W, hipStream_t s) {
         if (!u.level) { launch_op(u.first, B, H, W, s); return; }
+        static const bool dry = getenv("YH_LEVEL_DRYRUN") != nullptr;   // debugging: plan, never launch
+        if (dry) return;
         LevelArgs a{};
         a.ops = cur_plan->lops_dev + u.lop_off;
         a.nops = u.lop_cnt;
@@ -1063,6 +1084,8 @@ struct Net {
         static const int skip = [] { const char* e = getenv("YH_LEVEL_SKIP"); return e ? atoi(e) : 0; }();
         a.skip = skip;
         a.trace = level_trace_ptr ? level_trace_ptr + 8 * u.lop_off : nullptr;
+        static const int plain_ok = [] { const char* e = getenv("YH_LEVEL_PLAIN"); return e ? atoi(e) : 1; }();
+        a.plain_ok = plain_ok;
         const int rc = launch_level(dtype, a, s);
         if (rc != 0) throw Fail(YH_EHIP, "level program launch (" + ops[u.first].label + " .. " + ops[u.last - 1].label +
                                          ") failed: " + hipGetErrorString((hipError_t)rc));

@@ -61,11 +61,17 @@ __device__ __forceinline__ uint4 ld16(__amdgpu_buffer_rsrc_t r, int off) {
 __device__ __forceinline__ uint2 ld8(__amdgpu_buffer_rsrc_t r, int off) {
     return __builtin_bit_cast(uint2, __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, SC1));
 }
-__device__ __forceinline__ void st16(__amdgpu_buffer_rsrc_t r, int off, uint4 v) {
-    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4i, v), r, off, 0, SC1);
+// Activation stores. sc1 stores write through and drop the line from the XCD's
+// L2, so a reader on any XCD fetches the new bytes; when every member of the
+// cluster runs on one XCD (checked at launch, g_plain) plain stores keep the line
+// in that shared L2, where the members' sc1 (L1-bypassing) loads find it.
+__device__ __forceinline__ void st16(__amdgpu_buffer_rsrc_t r, int off, uint4 v, bool plain) {
+    if (plain) __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4i, v), r, off, 0, 0);
+    else __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4i, v), r, off, 0, SC1);
 }
-__device__ __forceinline__ void st8(__amdgpu_buffer_rsrc_t r, int off, uint2 v) {
-    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(v2i, v), r, off, 0, SC1);
+__device__ __forceinline__ void st8(__amdgpu_buffer_rsrc_t r, int off, uint2 v, bool plain) {
+    if (plain) __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(v2i, v), r, off, 0, 0);
+    else __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(v2i, v), r, off, 0, SC1);
 }
 // Read-only operands (weights, biases, k-tables) whose pointers come from the op
 // descriptors in memory: load through global (address space 1) pointers so they
@@ -142,7 +148,7 @@ __device__ __forceinline__ void load_bias(const ConvArgs& p, int co, float (&bv)
 }
 template <typename T, int NT>
 __device__ __forceinline__ void conv_store(const ConvArgs& p, __amdgpu_buffer_rsrc_t R, int outo, int reso, int m,
-                                           int co, const f32x4 (&acc)[NT], const float (&bv)[4 * NT]) {
+                                           int co, const f32x4 (&acc)[NT], const float (&bv)[4 * NT], bool plain) {
     constexpr int RUN = 4 * NT;
     float v[RUN];
 #pragma unroll
@@ -164,7 +170,7 @@ __device__ __forceinline__ void conv_store(const ConvArgs& p, __amdgpu_buffer_rs
 #pragma unroll
                 for (int e = 0; e < 8; ++e) f[e] += g[e];
             }
-            st16(R, outo + (m * p.ldo + co + c8 * 8) * 2, f_to_u4<T>(f));
+            st16(R, outo + (m * p.ldo + co + c8 * 8) * 2, f_to_u4<T>(f), plain);
         }
     } else {
         float g[4] = {0.f, 0.f, 0.f, 0.f};
@@ -177,7 +183,7 @@ __device__ __forceinline__ void conv_store(const ConvArgs& p, __amdgpu_buffer_rs
         T o[4];
 #pragma unroll
         for (int e = 0; e < 4; ++e) o[e] = fromf<T>(p.res ? v[e] + g[e] : v[e]);
-        st8(R, outo + (m * p.ldo + co) * 2, *reinterpret_cast<const uint2*>(o));
+        st8(R, outo + (m * p.ldo + co) * 2, *reinterpret_cast<const uint2*>(o), plain);
     }
 }
 
@@ -188,7 +194,7 @@ __device__ __forceinline__ void conv_store(const ConvArgs& p, __amdgpu_buffer_rs
 // so each lane ends with 4*NT contiguous output channels of its pixel.
 template <typename T, int NT>
 __device__ __forceinline__ void conv_op(const ConvArgs& p, __amdgpu_buffer_rsrc_t R, const void* base, int n, int t0, int t1,
-                        const int* kt, int wave, int lane) {
+                        const int* kt, int wave, int lane, bool plain) {
     constexpr int RUN = 4 * NT;
     const int li = lane & 15, q = lane >> 4;
     const int P = p.Ho * p.Wo;
@@ -243,7 +249,7 @@ __device__ __forceinline__ void conv_op(const ConvArgs& p, __amdgpu_buffer_rsrc_
         if (!pv || co >= p.Cout) continue;
         float bv[RUN];
         load_bias<T, NT>(p, co, bv, 1 << 30, nullptr);
-        conv_store<T, NT>(p, R, outo, reso, pix, co, acc, bv);
+        conv_store<T, NT>(p, R, outo, reso, pix, co, acc, bv, plain);
     }
 }
 
@@ -264,7 +270,7 @@ __device__ __forceinline__ void conv_op(const ConvArgs& p, __amdgpu_buffer_rsrc_
 template <typename T, int NT>
 __device__ __forceinline__ void conv_patch(const LevelOp& op, __amdgpu_buffer_rsrc_t R, const void* base, int n, int p0,
                                            int p1, int ch0, int ch1, const int* koff, char* lds, int wave, int lane,
-                                           unsigned long long* tr, int* err) {
+                                           unsigned long long* tr, int* err, bool plain) {
     const ConvArgs& p = op.c;
     constexpr int RUN = 4 * NT;
     const int ps = op.pstride, wp = op.wp, nck = p.Cin / 8;
@@ -404,7 +410,7 @@ __device__ __forceinline__ void conv_patch(const LevelOp& op, __amdgpu_buffer_rs
 #pragma unroll
         for (int j = 0; j < LP_MT; ++j) {
             const int pix = (mb + j) * 16 + li;
-            if (j < mt && pix < q1 && co < p.Cout) conv_store<T, NT>(p, R, outo, reso, pix, co, acc[j], bv);
+            if (j < mt && pix < q1 && co < p.Cout) conv_store<T, NT>(p, R, outo, reso, pix, co, acc[j], bv, plain);
         }
     }
 }
@@ -415,7 +421,8 @@ __device__ __forceinline__ void conv_patch(const LevelOp& op, __amdgpu_buffer_rs
 // any is used (out-of-image taps read zeros: adding w*0 to the fp32 sum leaves it
 // bit-identical to skipping the tap, as dwconv3x3 does).
 template <typename T>
-__device__ __forceinline__ void dw_op(const DwArgs& p, __amdgpu_buffer_rsrc_t R, const void* base, int n, int p0, int p1) {
+__device__ __forceinline__ void dw_op(const DwArgs& p, __amdgpu_buffer_rsrc_t R, const void* base, int n, int p0, int p1,
+                                      bool plain) {
     const int cpp = p.C / 8, HW = p.H * p.W;
     const int ino = boff(p.in, base) + n * (HW * p.ldi * 2);
     const int outo = boff(p.out, base) + n * (HW * p.ldo * 2);
@@ -448,7 +455,7 @@ __device__ __forceinline__ void dw_op(const DwArgs& p, __amdgpu_buffer_rsrc_t R,
             if (p.act == ACT_SILU) v = silu<T>(v);
             o[e] = v;
         }
-        st16(R, outo + (px * p.ldo + c0) * 2, f_to_u4<T>(o));
+        st16(R, outo + (px * p.ldo + c0) * 2, f_to_u4<T>(o), plain);
     }
 }
 
@@ -457,7 +464,8 @@ __device__ __forceinline__ void dw_op(const DwArgs& p, __amdgpu_buffer_rsrc_t R,
 // into slice step+1 (maxpool5 in misc.hip, nets/nn.py:90-94). The 25 taps of a
 // row of 5 are loaded together; out-of-image taps are masked out of the max.
 template <typename T>
-__device__ __forceinline__ void pool_op(const PoolArgs& p, int step, __amdgpu_buffer_rsrc_t R, const void* base, int n, int p0, int p1) {
+__device__ __forceinline__ void pool_op(const PoolArgs& p, int step, __amdgpu_buffer_rsrc_t R, const void* base, int n, int p0,
+                                        int p1, bool plain) {
     const int cpp = p.C / 8, HW = p.H * p.W;
     const int img = boff(p.buf, base) + n * (HW * p.ldc * 2);
     const int src = img + step * p.C * 2, dst = img + (step + 1) * p.C * 2;
@@ -487,7 +495,7 @@ __device__ __forceinline__ void pool_op(const PoolArgs& p, int step, __amdgpu_bu
                 for (int e = 0; e < 8; ++e) mx[e] = ok[k] ? fmaxf(mx[e], f[e]) : mx[e];
             }
         }
-        st16(R, dst + (px * p.ldc + c0) * 2, f_to_u4<T>(mx));
+        st16(R, dst + (px * p.ldc + c0) * 2, f_to_u4<T>(mx), plain);
     }
 }
 
@@ -518,7 +526,7 @@ __device__ __forceinline__ s16x4 lds_tr16(const void* p) {
 // positional dwconv pe(v) + bias of those 16 pixels (pe_add), all in registers.
 template <typename T>
 __device__ __forceinline__ void attn_tile(const AttnArgs& p, __amdgpu_buffer_rsrc_t R, const void* base, int n, int head, int q0,
-                          T* vl, int lane) {
+                          T* vl, int lane, bool plain) {
     const int g = lane >> 4, li = lane & 15;
     const int per = 2 * ADK + ADH;
     const int qkv = boff(p.qkv, base) + n * (p.T * p.ldq * 2) + head * per * 2;
@@ -617,7 +625,7 @@ __device__ __forceinline__ void attn_tile(const AttnArgs& p, __amdgpu_buffer_rsr
         T ov[4];
 #pragma unroll
         for (int r = 0; r < 4; ++r) ov[r] = fromf<T>(acc[t][r]);
-        st8(R, outo + (16 * t + 4 * g) * 2, *reinterpret_cast<const uint2*>(ov));
+        st8(R, outo + (16 * t + 4 * g) * 2, *reinterpret_cast<const uint2*>(ov), plain);
     }
 }
 
@@ -633,6 +641,24 @@ __global__ __launch_bounds__(LP_T) void level_program(const LevelArgs a, const L
     unsigned* gen = cnt + 32;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const __amdgpu_buffer_rsrc_t R = make_rsrc(a.base);
+    // Placement check: do all members of this cluster run on one XCD?
+    __shared__ int s_plain;
+    {
+        unsigned* xcc_slot = a.bar + 32 * 64 + cl * 32;
+        if (threadIdx.x == 0)
+            __hip_atomic_store(xcc_slot + member, __builtin_amdgcn_s_getreg((3 << 11) | 20) & 0xfu, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+        cluster_barrier(cnt, gen, a.G, a.err);
+        if (threadIdx.x == 0) {
+            const unsigned x0 = __hip_atomic_load(xcc_slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            int same = a.plain_ok;
+            for (int m = 1; m < a.G; ++m)
+                same &= __hip_atomic_load(xcc_slot + m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == x0;
+            s_plain = same;
+        }
+        __syncthreads();
+    }
+    const bool plain = s_plain != 0;
     const int npass = (a.B + a.NC - 1) / a.NC;
     for (int pass = 0; pass < npass; ++pass) {
         const int n = pass * a.NC + cl;
@@ -672,34 +698,34 @@ __global__ __launch_bounds__(LP_T) void level_program(const LevelArgs a, const L
                         const int p0 = mp * npt / pm * 16, p1 = min(P, (mp + 1) * npt / pm * 16);
                         if (tr) tr[2] = __builtin_amdgcn_s_memrealtime();
                         if (p1 > p0 && ch1 > ch0) {
-                            if (op.nt == 4) conv_patch<T, 4>(op, R, a.base, n, p0, p1, ch0, ch1, ktab, patch_lds, wave, lane, tr, a.err);
-                            else if (op.nt == 2) conv_patch<T, 2>(op, R, a.base, n, p0, p1, ch0, ch1, ktab, patch_lds, wave, lane, tr, a.err);
-                            else conv_patch<T, 1>(op, R, a.base, n, p0, p1, ch0, ch1, ktab, patch_lds, wave, lane, tr, a.err);
+                            if (op.nt == 4) conv_patch<T, 4>(op, R, a.base, n, p0, p1, ch0, ch1, ktab, patch_lds, wave, lane, tr, a.err, plain);
+                            else if (op.nt == 2) conv_patch<T, 2>(op, R, a.base, n, p0, p1, ch0, ch1, ktab, patch_lds, wave, lane, tr, a.err, plain);
+                            else conv_patch<T, 1>(op, R, a.base, n, p0, p1, ch0, ch1, ktab, patch_lds, wave, lane, tr, a.err, plain);
                         }
                     } else {
                         for (int i = threadIdx.x; i < KTAB_MAX; i += LP_T) ktab[i] = i < kc8 ? ldgi(c.ktab + i) : 0xffff;
                         __syncthreads();
                         const int t0 = member * npt / a.G, t1 = (member + 1) * npt / a.G;
-                        if (op.nt == 4) conv_op<T, 4>(c, R, a.base, n, t0, t1, ktab, wave, lane);
-                        else if (op.nt == 2) conv_op<T, 2>(c, R, a.base, n, t0, t1, ktab, wave, lane);
-                        else conv_op<T, 1>(c, R, a.base, n, t0, t1, ktab, wave, lane);
+                        if (op.nt == 4) conv_op<T, 4>(c, R, a.base, n, t0, t1, ktab, wave, lane, plain);
+                        else if (op.nt == 2) conv_op<T, 2>(c, R, a.base, n, t0, t1, ktab, wave, lane, plain);
+                        else conv_op<T, 1>(c, R, a.base, n, t0, t1, ktab, wave, lane, plain);
                     }
                 } else if (kind == LOP_DW) {
                     const DwArgs d = opp->d;
                     const int P = d.H * d.W, npt = (P + 15) / 16;
                     const int p0 = member * npt / a.G * 16, p1 = min(P, (member + 1) * npt / a.G * 16);
-                    dw_op<T>(d, R, a.base, n, p0, p1);
+                    dw_op<T>(d, R, a.base, n, p0, p1, plain);
                 } else if (kind == LOP_POOL) {
                     const PoolArgs pl = opp->pl;
                     const int step = opp->step;
                     const int P = pl.H * pl.W, npt = (P + 15) / 16;
                     const int p0 = member * npt / a.G * 16, p1 = min(P, (member + 1) * npt / a.G * 16);
-                    pool_op<T>(pl, step, R, a.base, n, p0, p1);
+                    pool_op<T>(pl, step, R, a.base, n, p0, p1, plain);
                 } else {
                     const AttnArgs at = opp->at;
                     const int qt = (at.T + 15) / 16, tasks = at.heads * qt;
                     for (int tk = member * LP_W + wave; tk < tasks; tk += a.G * LP_W)
-                        attn_tile<T>(at, R, a.base, n, tk / qt, (tk % qt) * 16, vlds[wave], lane);
+                        attn_tile<T>(at, R, a.base, n, tk / qt, (tk % qt) * 16, vlds[wave], lane, plain);
                 }
             }
             if (tr) tr[5] = __builtin_amdgcn_s_memrealtime();
@@ -721,15 +747,28 @@ __global__ __launch_bounds__(LP_T) void level_program(const LevelArgs a, const L
 int launch_level(int dtype, const LevelArgs& a, hipStream_t s) {
     if (a.NC % 8 != 0 || a.G <= 0 || a.nops <= 0) return (int)hipErrorInvalidValue;
     const dim3 grid(a.NC * a.G);
-    static bool attr = false;
-    if (!attr) {
-        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&level_program<_Float16>),
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, 136 * 1024);
-        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&level_program<__bf16>),
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, 136 * 1024);
-        attr = true;
+    // dynamic LDS limit = per-workgroup opt-in maximum minus the kernel's static LDS
+    static int max_dyn = -1;
+    if (max_dyn < 0) {
+        int dev = 0, optin = 0;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&optin, hipDeviceAttributeSharedMemPerBlockOptin, dev) != hipSuccess)
+            return (int)hipErrorInvalidValue;
+        hipFuncAttributes fa16{}, fa16b{};
+        if (hipFuncGetAttributes(&fa16, reinterpret_cast<const void*>(&level_program<_Float16>)) != hipSuccess ||
+            hipFuncGetAttributes(&fa16b, reinterpret_cast<const void*>(&level_program<__bf16>)) != hipSuccess)
+            return (int)hipErrorInvalidValue;
+        const int st = (int)(fa16.sharedSizeBytes > fa16b.sharedSizeBytes ? fa16.sharedSizeBytes : fa16b.sharedSizeBytes);
+        max_dyn = optin - st;
+        if (hipFuncSetAttribute(reinterpret_cast<const void*>(&level_program<_Float16>),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, max_dyn) != hipSuccess ||
+            hipFuncSetAttribute(reinterpret_cast<const void*>(&level_program<__bf16>),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, max_dyn) != hipSuccess) {
+            max_dyn = 0;
+            return (int)hipErrorInvalidValue;
+        }
     }
-    if (a.lds_patch > 136 * 1024) return (int)hipErrorInvalidValue;
+    if (a.lds_patch > max_dyn) return (int)hipErrorInvalidValue;
     switch (dtype) {
         case F16: hipLaunchKernelGGL((level_program<_Float16>), grid, dim3(LP_T), a.lds_patch, s, a, a.ops); break;
         case BF16: hipLaunchKernelGGL((level_program<__bf16>), grid, dim3(LP_T), a.lds_patch, s, a, a.ops); break;
