@@ -5,6 +5,9 @@
 // kernels (optionally as one captured HIP graph) and exports the C ABI
 // declared in include/yolo_hip.h.
 #include <hip/hip_runtime.h>
+#include <execinfo.h>
+#include <signal.h>
+#include <unistd.h>
 
 #include <algorithm>
 #include <cmath>
@@ -18,6 +21,17 @@
 
 #include "common.h"
 #include "yolo_hip.h"
+
+// YH_SEGV_BT=1 (debugging): print a native backtrace on SIGSEGV before the
+// default handler runs, so a host-side crash inside a call names its frame
+static void segv_bt(int sig) {
+    void* fr[64];
+    const int n = backtrace(fr, 64);
+    (void)!write(2, "[yh] native backtrace:\n", 23);
+    backtrace_symbols_fd(fr, n, 2);
+    signal(sig, SIG_DFL);
+    raise(sig);
+}
 
 static unsigned long long* level_trace_ptr = nullptr;   // yh_debug_level_trace
 
@@ -1091,6 +1105,127 @@ struct Net {
                                          ") failed: " + hipGetErrorString((hipError_t)rc));
     }
 
+    // ---------------------------------------------------------- parallel capture
+    // The forward is a DAG (C3k's two 1x1 branches, the head's box / cls chains,
+    // the 80x80 head beside the FPN's bottom-up path, ...). When the forward is
+    // captured as a HIP graph, launch units are spread over up to par_streams
+    // streams joined by events, so the graph gets the DAG's edges and independent
+    // small kernels run side by side instead of back to back.
+    // Opt-in (YH_STREAMS=N): worth ~6 % at v11_n b32 bf16, but hipGraphLaunch of some
+    // multi-branch graphs segfaults inside libamdhip64 (ROCm 7; e.g. fp16 b4 with every
+    // conv forced to conv_stream<4 slots>), so the default keeps one stream.
+    int par_streams = [] { const char* e = getenv("YH_STREAMS"); return e ? std::max(1, std::min(8, atoi(e))) : 1; }();
+    std::vector<hipStream_t> aux_streams;
+    std::vector<hipEvent_t> unit_events;
+    struct Rg { int t, c0, c1; };
+    void unit_regions(const Unit& u, std::vector<Rg>& rd, std::vector<Rg>& wr) const {
+        for (int k = u.first; k < u.last; ++k) {
+            const Op& op = ops[k];
+            for (auto& sg : op.in) rd.push_back({sg.v.t, sg.v.coff, sg.v.coff + sg.v.C});
+            if (op.has_res) rd.push_back({op.res.t, op.res.coff, op.res.coff + op.res.C});
+            if (op.kind == OP_DECODE) {
+                for (int l = 0; l < 3; ++l) rd.push_back({op.lvl[l].t, 0, tensors[op.lvl[l].t].C});
+                wr.push_back({-2, 0, 1});   // the caller's y
+            } else if (op.kind == OP_SPPF) {
+                rd.push_back({op.out.t, op.out.coff, op.out.coff + op.out.C});
+                wr.push_back({op.out.t, op.out.coff + op.out.C, op.out.coff + 4 * op.out.C});
+            } else {
+                wr.push_back({op.out.t, op.out.coff, op.out.coff + op.out.C});
+            }
+            if (op.kind == OP_FIRST) rd.push_back({-1, 0, 1});   // the caller's x
+        }
+    }
+    void release_unit_events() {
+        for (auto e : unit_events) (void)hipEventDestroy(e);
+        unit_events.clear();
+    }
+    void run_units_parallel(int B, int H, int W, hipStream_t origin) {
+        const auto& us = cur_plan->units;
+        const int n = (int)us.size();
+        const int NS = par_streams;
+        while ((int)aux_streams.size() < NS - 1) {
+            hipStream_t st;
+            HIPCHECK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+            aux_streams.push_back(st);
+        }
+        // fresh events per capture: HIP keeps a reference to the capture node an event
+        // was recorded at, so reusing one in a later capture (after that graph was
+        // destroyed) dereferences a dead node. forward() destroys them after EndCapture.
+        release_unit_events();
+        for (int i = 0; i < n + NS; ++i) {
+            hipEvent_t e;
+            HIPCHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+            unit_events.push_back(e);
+        }
+        // dependencies (RAW / WAR / WAW on channel ranges)
+        std::vector<std::vector<Rg>> rd(n), wr(n);
+        for (int i = 0; i < n; ++i) unit_regions(us[i], rd[i], wr[i]);
+        auto ov = [](const std::vector<Rg>& a, const std::vector<Rg>& b) {
+            for (auto& x : a)
+                for (auto& y : b)
+                    if (x.t == y.t && x.c0 < y.c1 && y.c0 < x.c1) return true;
+            return false;
+        };
+        std::vector<std::vector<int>> preds(n);
+        std::vector<std::vector<char>> anc(n, std::vector<char>(n, 0));   // anc[j][i]: i is an ancestor of j
+        for (int j = 0; j < n; ++j)
+            for (int i = 0; i < j; ++i)
+                if (ov(wr[i], rd[j]) || ov(rd[i], wr[j]) || ov(wr[i], wr[j])) {
+                    preds[j].push_back(i);
+                    anc[j][i] = 1;
+                    for (int k = 0; k < i; ++k) anc[j][k] |= anc[i][k];
+                }
+        // fork: every stream starts after the origin's prior work
+        std::vector<hipStream_t> st(NS);
+        st[0] = origin;
+        for (int k = 1; k < NS; ++k) st[k] = aux_streams[k - 1];
+        hipEvent_t fork = unit_events[n];
+        HIPCHECK(hipEventRecord(fork, origin));
+        for (int k = 1; k < NS; ++k) HIPCHECK(hipStreamWaitEvent(st[k], fork, 0));
+        std::vector<int> last(NS, -1);
+        std::vector<int> where(n, 0);
+        for (int j = 0; j < n; ++j) {
+            // a stream whose last unit is an ancestor adds no false dependency; prefer
+            // continuing a direct predecessor's chain, then an idle stream
+            int pick = -1, score = -1;
+            for (int k = 0; k < NS; ++k) {
+                int sc;
+                if (last[k] < 0) sc = 1;
+                else if (anc[j][last[k]]) sc = std::find(preds[j].begin(), preds[j].end(), last[k]) != preds[j].end() ? 3 : 2;
+                else sc = 0;
+                if (sc > score) { score = sc; pick = k; }
+            }
+            if (score == 0) {   // every stream is busy with concurrent work: join the oldest
+                pick = 0;
+                for (int k = 1; k < NS; ++k)
+                    if (last[k] < last[pick]) pick = k;
+            }
+            // wait for predecessors on other streams not already implied by stream order
+            std::vector<int> latest(NS, -1);
+            for (int i : preds[j]) {
+                const int si = where[i];
+                if (si == pick) continue;
+                if (last[pick] >= 0 && (last[pick] == i || anc[last[pick]][i])) continue;
+                latest[si] = std::max(latest[si], i);
+            }
+            for (int k = 0; k < NS; ++k)
+                if (latest[k] >= 0) HIPCHECK(hipStreamWaitEvent(st[pick], unit_events[latest[k]], 0));
+            launch_unit(us[j], B, H, W, st[pick]);
+            HIPCHECK(hipEventRecord(unit_events[j], st[pick]));
+            where[j] = pick;
+            last[pick] = j;
+        }
+        // join every stream back into the origin
+        for (int k = 1; k < NS; ++k) {
+            if (last[k] < 0) {   // unused stream: still has to rejoin the capture
+                HIPCHECK(hipEventRecord(unit_events[n + k], st[k]));
+            } else {
+                HIPCHECK(hipEventRecord(unit_events[n + k], st[k]));
+            }
+            HIPCHECK(hipStreamWaitEvent(origin, unit_events[n + k], 0));
+        }
+    }
+
     void run_ops(int B, int H, int W, hipStream_t s) {
         if (!cur_plan) {
             for (size_t i = 0; i < ops.size(); ++i) launch_op(i, B, H, W, s);
@@ -1100,6 +1235,13 @@ struct Net {
     }
 
     void forward(const void* x, int B, int H, int W, void* y, hipStream_t s) {
+        static const bool bt = getenv("YH_SEGV_BT") != nullptr;
+        if (bt) {
+            struct sigaction sa {};
+            sa.sa_handler = segv_bt;
+            sa.sa_flags = SA_RESETHAND;
+            sigaction(SIGSEGV, &sa, nullptr);
+        }
         for (auto& d : convs) require(d.loaded, "weights of " + d.name + " not loaded", YH_ESTATE);
         reserve(B, H, W);
         HIPCHECK(hipSetDevice(device));
@@ -1144,15 +1286,21 @@ struct Net {
             hipGraph_t g = nullptr;
             HIPCHECK(hipStreamBeginCapture(cap_stream, hipStreamCaptureModeThreadLocal));
             try {
-                run_ops(B, H, W, cap_stream);
+                if (par_streams > 1) run_units_parallel(B, H, W, cap_stream);
+                else run_ops(B, H, W, cap_stream);
             } catch (...) {
                 (void)hipStreamEndCapture(cap_stream, &g);
+                release_unit_events();
                 if (g) (void)hipGraphDestroy(g);
                 throw;
             }
+            if (bt) fprintf(stderr, "[yh] captured B=%d H=%d W=%d streams=%d\n", B, H, W, par_streams);
             HIPCHECK(hipStreamEndCapture(cap_stream, &g));
+            release_unit_events();
+            if (bt) fprintf(stderr, "[yh] capture ended\n");
             hipGraphExec_t ex = nullptr;
             HIPCHECK(hipGraphInstantiate(&ex, g, nullptr, nullptr, 0));
+            if (bt) fprintf(stderr, "[yh] instantiated\n");
             (void)hipGraphDestroy(g);
             it = graphs.emplace(key, ex).first;
         }
@@ -1239,6 +1387,8 @@ struct Net {
         if (io_dev) (void)hipFree(io_dev);
         if (zero_dev) (void)hipFree(zero_dev);
         if (cap_stream) (void)hipStreamDestroy(cap_stream);
+        for (auto st : aux_streams) (void)hipStreamDestroy(st);
+        release_unit_events();
         for (auto e : ev) (void)hipEventDestroy(e);
     }
 };
