@@ -73,10 +73,17 @@ def roofline(eng, args, batch, prof_steps, x, y):
             f"{c['bytes'] / c['ms'] / 1e6:7.0f} GB/s  {c['flops'] / c['ms'] / 1e9:7.1f} TFLOP/s  "
             f"attainable {100 * c['attain_ms'] / c['ms']:4.1f}%")
     dom = by_cls["conv3x3"]
-    achieved = dom["bytes"] / dom["ms"] / 1e6  # GB/s
-    traffic, traffic_src = pmc_traffic("conv3x3")
-    return dict(bound="hbm", achieved=round(achieved, 1), peak=HBM_PEAK_GBS, unit="GB/s",
-                frac=round(achieved / HBM_PEAK_GBS, 4), traffic=traffic, traffic_source=traffic_src,
+    # the family's binding roof: HBM below the ridge (v11_n/s at 640), MFMA above (v11_x at 1280)
+    peak_tf = MFMA_PEAK_TFLOPS[args.dtype]
+    mfma_bound = dom["flops"] / (peak_tf * 1e12) > dom["bytes"] / (HBM_PEAK_GBS * 1e9)
+    if mfma_bound:
+        achieved, peak, unit, bound = dom["flops"] / dom["ms"] / 1e9, peak_tf, "TFLOP/s", "mfma"
+    else:
+        achieved, peak, unit, bound = dom["bytes"] / dom["ms"] / 1e6, HBM_PEAK_GBS, "GB/s", "hbm"
+    traffic, traffic_src = pmc_traffic("conv3x3", args)
+    return dict(bound=bound, achieved=round(achieved, 1), peak=peak, unit=unit,
+                frac=round(achieved / peak, 4), traffic=traffic, traffic_source=traffic_src,
+                algorithmic_flops_per_launch=round(dom["flops"] / dom["launches"]),
                 kernel="dense 3x3 convs: conv_direct / conv_gemm2 / conv_stream implicit-GEMM MFMA, autotuned per layer",
                 launches_per_step=dom["launches"],
                 avg_launch_us=round(dom["ms"] * 1e3 / dom["launches"], 2),
@@ -88,13 +95,17 @@ def roofline(eng, args, batch, prof_steps, x, y):
 PMC_SUMMARY = os.path.join(ROOT, "profiles", "pmc_traffic_latest.json")
 
 
-def pmc_traffic(cls):
+def pmc_traffic(cls, args):
     """HBM bytes per launch of kernel family `cls` from the committed rocprofv3 PMC summary
     (FETCH_SIZE / WRITE_SIZE passes over tools/pmc_run.py, corrected per the gfx950 guide by
-    tools/pmc_traffic.py); bench.py cannot collect PMC counters from inside its own process."""
+    tools/pmc_traffic.py); bench.py cannot collect PMC counters from inside its own process.
+    None unless the summary was collected on this bench's configuration."""
     try:
         with open(PMC_SUMMARY) as f:
             rec = json.load(f)
+        cfg = rec.get("config", {"variant": "n", "size": 640, "batch": 32, "dtype": "bf16"})
+        if (cfg["variant"], cfg["size"], cfg["batch"], cfg["dtype"]) != (args.variant, args.size, args.batch, args.dtype):
+            return None, None
         fam = rec["family"][cls]
         return round(fam["traffic_per_launch"]), (f"{os.path.relpath(PMC_SUMMARY, ROOT)}: {rec['source']}; "
                                                   f"{rec['corrections']}; {fam['traffic_over_alg']:.2f}x algorithmic")
@@ -219,7 +230,7 @@ def main():
         imgs = B * world * args.steps
         value = imgs / elapsed
         rec = {
-            "metric": "images/sec at 640x640 batch32, v11_n (forward + on-device NMS)",
+            "metric": f"images/sec at {S}x{S} batch{B}, v11_{args.variant} (forward + on-device NMS)",
             "value": round(value, 2),
             "unit": "images/s",
             "n_gpus": world,

@@ -70,7 +70,9 @@ def main():
                         traffic_per_launch=sum(r["traffic"] for r in rows) / len(rows),
                         alg_bytes_per_launch=sum(r["alg_bytes"] for r in rows) / len(rows),
                         traffic_over_alg=sum(r["traffic"] for r in rows) / sum(r["alg_bytes"] for r in rows))
-    rec = dict(source="rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of tools/pmc_run.py",
+    cfg = dict(variant=os.environ.get("YH_VARIANT", "n"), size=int(os.environ.get("YH_SIZE", "640")),
+               batch=int(os.environ.get("YH_BATCH", "32")), dtype="bf16")
+    rec = dict(config=cfg, source="rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of tools/pmc_run.py",
                corrections="KiB x1024; FETCH_SIZE x2 (gfx950 wide-read half count)", family=fam, ops=per_op)
     for cls, v in fam.items():
         print(f"{cls}: {v['launches']} launches, traffic {v['traffic_per_launch'] / 1e6:.2f} MB/launch vs "
