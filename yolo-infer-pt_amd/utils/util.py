@@ -5,6 +5,9 @@
   non_max_suppression   reference utils/util.py:123-169, run on device by the gfx950
                         kernels behind include/yolo_hip.h (yh_nms)
   setup_seed            reference utils/util.py:12-20
+  load_weight           reference utils/util.py:345-355 } yolo_hip.weights: safe checkpoint
+  load_ultralytics_weight  utils/util.py:358-516       } reading + key mapping; the HIP
+                        engine re-packs the new parameters on the next device forward
 
 non_max_suppression semantics: candidate (anchor, class) pairs with score >
 threshold (compared in the tensor dtype), score-descending order with ties
@@ -20,7 +23,8 @@ import random
 import numpy
 import torch
 
-__all__ = ["setup_seed", "wh2xy", "make_anchors", "non_max_suppression"]
+__all__ = ["setup_seed", "wh2xy", "make_anchors", "non_max_suppression", "load_weight",
+           "load_ultralytics_weight"]
 
 MAX_WH = 7680
 MAX_DET = 300
@@ -71,3 +75,15 @@ def non_max_suppression(outputs, confidence_threshold=0.001, iou_threshold=0.65)
     dets, counts = nms(outputs, confidence_threshold, iou_threshold, MAX_DET, MAX_NMS, float(MAX_WH))
     kept = counts.tolist()
     return [dets[i, :k].to(outputs.dtype) for i, k in enumerate(kept)]
+
+
+def load_weight(model, ckpt, trusted=False):
+    """Keep the checkpoint tensors whose key and shape match the model; load non-strictly."""
+    from yolo_hip.weights import load_weight as _lw
+    return _lw(model, ckpt, trusted=trusted)
+
+
+def load_ultralytics_weight(model, ckpt_path, mapping="reference", trusted=False):
+    """Ultralytics YOLO11 checkpoint -> model (mapping "reference" = the reference's key map, "exact" = all keys)."""
+    from yolo_hip.weights import load_ultralytics_weight as _lu
+    return _lu(model, ckpt_path, mapping=mapping, trusted=trusted)
