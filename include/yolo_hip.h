@@ -14,6 +14,7 @@
  *   yh_load_conv        nets/nn.py:8-25     fuse_conv (BN folded into conv in fp32), nets/nn.py:299-305 YOLO.fuse
  *   yh_forward          nets/nn.py:294-297  YOLO.forward in eval mode, incl. Head.forward decode
  *                       (nets/nn.py:255-270), DFL (nets/nn.py:222-225) and make_anchors (utils/util.py:85-96)
+ *   yh_forward_u8       main.py:265-267     uint8 -> dtype, / 255 preprocessing fused into yh_forward's stem
  *   yh_nms              utils/util.py:123-169 non_max_suppression (+ torchvision.ops.nms, util.py:162)
  *
  * Conventions
@@ -113,6 +114,15 @@ int yh_reserve(yh_handle* h, int batch, int height, int width);
  * height, width: multiples of 32. */
 int yh_forward(yh_handle* h, const void* x, int batch, int height, int width,
                void* y, void* stream);
+
+/* yh_forward on the data loader's image tensor: x is device (batch, 3, height,
+ * width) NCHW uint8 (RGB, utils/dataset.py:86-88 layout), and the reference's
+ * preprocessing `samples.half() / 255.` (main.py:265-267; to the handle dtype)
+ * is fused into the stem's input load - no converted copy of x is made.
+ * Bit-identical to yh_forward on x.to(dtype) / 255. computed by torch on the
+ * device (u * fp32(1/255), rounded to the dtype). */
+int yh_forward_u8(yh_handle* h, const void* x, int batch, int height, int width,
+                  void* y, void* stream);
 
 /* Bytes of device workspace yh_nms needs for a (batch, 4 + num_classes, anchors) input. */
 size_t yh_nms_workspace_bytes(int batch, int num_classes, int anchors);

@@ -18,7 +18,7 @@ def header_symbols():
 
 def test_header_declares_the_boundary():
     syms = header_symbols()
-    for s in ("yh_create", "yh_destroy", "yh_load_conv", "yh_forward", "yh_nms", "yh_last_error"):
+    for s in ("yh_create", "yh_destroy", "yh_load_conv", "yh_forward", "yh_forward_u8", "yh_nms", "yh_last_error"):
         assert s in syms
 
 

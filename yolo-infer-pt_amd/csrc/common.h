@@ -41,6 +41,8 @@ struct FirstConvArgs {
     const float* bias;   // [Cout]
     void* out;
     int act;
+    int in_u8;           // 1: x is uint8 (the loader's image tensor); the kernel applies
+                         //    main.py:265-267's `x.to(dtype) / 255` while staging it
 };
 
 // Depthwise 3x3 stride-1 conv on an NHWC view.

@@ -1056,11 +1056,32 @@ int launch_conv_bm(int BM, int BN, const ConvArgs& a, hipStream_t s) {
 constexpr int STEM_TW = 128;
 constexpr int STEM_SEG = 2 * STEM_TW + 16;  // staged columns per row segment (aligned window)
 
-template <typename T, int NC8>
+// Input element U -> the value the stem sees. U == T: the caller's tensor as is.
+// U == uint8_t: the reference's preprocessing (main.py:265-267, `samples.half()
+// / 255.`) fused into the load, computed the way torch's device kernel does a
+// division by a CPU scalar: u (exact in T) times the fp32 reciprocal 1/255,
+// rounded to T.
+template <typename U, typename T>
+__device__ __forceinline__ float stem_in(U v) {
+    if constexpr (sizeof(U) == 1) return fromf_round<T>((float)v * (1.0f / 255.0f));
+    else return tof(v);
+}
+template <typename U, typename T>
+__device__ __forceinline__ void stem_in8(const U* p, float (&f)[8]) {
+    if constexpr (sizeof(U) == 1) {
+        const uint2 v = *reinterpret_cast<const uint2*>(p);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) f[e] = stem_in<uint8_t, T>((uint8_t)(((e < 4 ? v.x : v.y) >> (8 * (e & 3))) & 255u));
+    } else {
+        chunk_to_f(ld_chunk(p), f);
+    }
+}
+
+template <typename T, typename U, int NC8>
 __global__ __launch_bounds__(STEM_TW) void conv_first(const FirstConvArgs p) {
     __shared__ float patch[9][STEM_SEG];
     const int wo0 = blockIdx.x * STEM_TW, ho = blockIdx.y, n = blockIdx.z;
-    const T* x = reinterpret_cast<const T*>(p.io[0]);
+    const U* x = reinterpret_cast<const U*>(p.io[0]);
     const long long plane = (long long)p.H * p.W;
     const int col0 = 2 * wo0 - 8;  // 16-B aligned window start (8 elements before the first tap)
     constexpr int CPS = STEM_SEG / 8;
@@ -1071,13 +1092,13 @@ __global__ __launch_bounds__(STEM_TW) void conv_first(const FirstConvArgs p) {
         const int col = col0 + ch * 8;
         float f[8];
         if (hi >= 0 && hi < p.H && col >= 0 && col + 8 <= p.W) {
-            chunk_to_f(ld_chunk(x + ((long long)n * 3 + ci) * plane + (long long)hi * p.W + col), f);
+            stem_in8<U, T>(x + ((long long)n * 3 + ci) * plane + (long long)hi * p.W + col, f);
         } else {
 #pragma unroll
             for (int e = 0; e < 8; ++e) {
                 const int cc = col + e;
                 f[e] = (hi >= 0 && hi < p.H && cc >= 0 && cc < p.W)
-                           ? tof(x[((long long)n * 3 + ci) * plane + (long long)hi * p.W + cc]) : 0.f;
+                           ? stem_in<U, T>(x[((long long)n * 3 + ci) * plane + (long long)hi * p.W + cc]) : 0.f;
             }
         }
 #pragma unroll
@@ -1117,11 +1138,11 @@ __global__ __launch_bounds__(STEM_TW) void conv_first(const FirstConvArgs p) {
 // 16-bit stem on MFMA: K = 27 taps padded to 32 = one v_mfma_f32_16x16x32 per
 // 16 pixels x 16 couts. A = weights (built once per wave from the fp32 [27][Cout]
 // pack), B = the im2col column of 16 pixels gathered from the LDS patch.
-template <typename T, int NT>
+template <typename T, typename U, int NT>
 __global__ __launch_bounds__(STEM_TW) void conv_first_mfma(const FirstConvArgs p) {
     __shared__ float patch[9][STEM_SEG];
     const int wo0 = blockIdx.x * STEM_TW, ho = blockIdx.y, n = blockIdx.z;
-    const T* x = reinterpret_cast<const T*>(p.io[0]);
+    const U* x = reinterpret_cast<const U*>(p.io[0]);
     const long long plane = (long long)p.H * p.W;
     const int col0 = 2 * wo0 - 8;
     constexpr int CPS = STEM_SEG / 8;
@@ -1132,13 +1153,13 @@ __global__ __launch_bounds__(STEM_TW) void conv_first_mfma(const FirstConvArgs p
         const int col = col0 + ch * 8;
         float f[8];
         if (hi >= 0 && hi < p.H && col >= 0 && col + 8 <= p.W) {
-            chunk_to_f(ld_chunk(x + ((long long)n * 3 + ci) * plane + (long long)hi * p.W + col), f);
+            stem_in8<U, T>(x + ((long long)n * 3 + ci) * plane + (long long)hi * p.W + col, f);
         } else {
 #pragma unroll
             for (int e = 0; e < 8; ++e) {
                 const int cc = col + e;
                 f[e] = (hi >= 0 && hi < p.H && cc >= 0 && cc < p.W)
-                           ? tof(x[((long long)n * 3 + ci) * plane + (long long)hi * p.W + cc]) : 0.f;
+                           ? stem_in<U, T>(x[((long long)n * 3 + ci) * plane + (long long)hi * p.W + cc]) : 0.f;
             }
         }
 #pragma unroll
@@ -1202,28 +1223,33 @@ __global__ __launch_bounds__(STEM_TW) void conv_first_mfma(const FirstConvArgs p
     }
 }
 
-template <typename T>
-int launch_first_t(const FirstConvArgs& a, int B, hipStream_t s) {
+template <typename T, typename U>
+int launch_first_tu(const FirstConvArgs& a, int B, hipStream_t s) {
     const dim3 grid((a.Wo + STEM_TW - 1) / STEM_TW, a.Ho, B);
     if constexpr (sizeof(T) == 2) {
         switch ((a.Cout + 15) / 16) {
-            case 1: hipLaunchKernelGGL((conv_first_mfma<T, 1>), grid, dim3(STEM_TW), 0, s, a); break;
-            case 2: hipLaunchKernelGGL((conv_first_mfma<T, 2>), grid, dim3(STEM_TW), 0, s, a); break;
-            case 4: hipLaunchKernelGGL((conv_first_mfma<T, 4>), grid, dim3(STEM_TW), 0, s, a); break;
-            case 6: hipLaunchKernelGGL((conv_first_mfma<T, 6>), grid, dim3(STEM_TW), 0, s, a); break;
+            case 1: hipLaunchKernelGGL((conv_first_mfma<T, U, 1>), grid, dim3(STEM_TW), 0, s, a); break;
+            case 2: hipLaunchKernelGGL((conv_first_mfma<T, U, 2>), grid, dim3(STEM_TW), 0, s, a); break;
+            case 4: hipLaunchKernelGGL((conv_first_mfma<T, U, 4>), grid, dim3(STEM_TW), 0, s, a); break;
+            case 6: hipLaunchKernelGGL((conv_first_mfma<T, U, 6>), grid, dim3(STEM_TW), 0, s, a); break;
             default: return (int)hipErrorInvalidValue;
         }
         return (int)hipGetLastError();
     }
     switch (a.Cout) {
-        case 16: hipLaunchKernelGGL((conv_first<T, 2>), grid, dim3(STEM_TW), 0, s, a); break;
-        case 24: hipLaunchKernelGGL((conv_first<T, 3>), grid, dim3(STEM_TW), 0, s, a); break;
-        case 32: hipLaunchKernelGGL((conv_first<T, 4>), grid, dim3(STEM_TW), 0, s, a); break;
-        case 64: hipLaunchKernelGGL((conv_first<T, 8>), grid, dim3(STEM_TW), 0, s, a); break;
-        case 96: hipLaunchKernelGGL((conv_first<T, 12>), grid, dim3(STEM_TW), 0, s, a); break;
+        case 16: hipLaunchKernelGGL((conv_first<T, U, 2>), grid, dim3(STEM_TW), 0, s, a); break;
+        case 24: hipLaunchKernelGGL((conv_first<T, U, 3>), grid, dim3(STEM_TW), 0, s, a); break;
+        case 32: hipLaunchKernelGGL((conv_first<T, U, 4>), grid, dim3(STEM_TW), 0, s, a); break;
+        case 64: hipLaunchKernelGGL((conv_first<T, U, 8>), grid, dim3(STEM_TW), 0, s, a); break;
+        case 96: hipLaunchKernelGGL((conv_first<T, U, 12>), grid, dim3(STEM_TW), 0, s, a); break;
         default: return (int)hipErrorInvalidValue;
     }
     return (int)hipGetLastError();
+}
+
+template <typename T>
+int launch_first_t(const FirstConvArgs& a, int B, hipStream_t s) {
+    return a.in_u8 ? launch_first_tu<T, uint8_t>(a, B, s) : launch_first_tu<T, T>(a, B, s);
 }
 
 template <typename T>

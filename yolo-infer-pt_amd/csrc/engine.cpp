@@ -130,8 +130,9 @@ struct Workspace {
 
 struct GraphKey {
     int B, H, W;
+    int X = 0;   // input kind of a captured forward graph: 0 = handle dtype, 1 = uint8
     bool operator<(const GraphKey& o) const {
-        return B != o.B ? B < o.B : (H != o.H ? H < o.H : W < o.W);
+        return B != o.B ? B < o.B : (H != o.H ? H < o.H : (W != o.W ? W < o.W : X < o.X));
     }
 };
 
@@ -708,6 +709,7 @@ struct Net {
                 a.bias = d.b_dev;
                 a.out = ptr(op.out);
                 a.act = d.act;
+                a.in_u8 = in_u8;
                 rc = launch_first_conv(dtype, a, B, s);
                 break;
             }
@@ -1234,7 +1236,9 @@ struct Net {
         for (auto& u : cur_plan->units) launch_unit(u, B, H, W, s);
     }
 
-    void forward(const void* x, int B, int H, int W, void* y, hipStream_t s) {
+    int in_u8 = 0;   // the current forward's input kind (see GraphKey::X)
+    void forward(const void* x, int B, int H, int W, void* y, hipStream_t s, int x_u8 = 0) {
+        in_u8 = x_u8;
         static const bool bt = getenv("YH_SEGV_BT") != nullptr;
         if (bt) {
             struct sigaction sa {};
@@ -1279,7 +1283,7 @@ struct Net {
             run_ops(B, H, W, s);
             return;
         }
-        const GraphKey key{B, H, W};
+        const GraphKey key{B, H, W, in_u8};
         auto it = graphs.find(key);
         if (it == graphs.end()) {
             if (!cap_stream) HIPCHECK(hipStreamCreateWithFlags(&cap_stream, hipStreamNonBlocking));
@@ -1520,6 +1524,15 @@ int yh_forward(yh_handle* h, const void* x, int batch, int height, int width, vo
         yh::require(batch > 0, "batch must be positive");
         HIPCHECK(hipSetDevice(h->net.device));
         h->net.forward(x, batch, height, width, y, (hipStream_t)stream);
+    });
+}
+
+int yh_forward_u8(yh_handle* h, const void* x, int batch, int height, int width, void* y, void* stream) {
+    return guarded([&] {
+        yh::require(h && x && y, "null argument");
+        yh::require(batch > 0, "batch must be positive");
+        HIPCHECK(hipSetDevice(h->net.device));
+        h->net.forward(x, batch, height, width, y, (hipStream_t)stream, 1);
     });
 }
 

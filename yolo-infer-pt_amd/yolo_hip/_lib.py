@@ -40,6 +40,7 @@ _PROTOS = {
     "yh_workspace_bytes": (c_int, [c_void_p, c_int, c_int, c_int, POINTER(c_size_t)]),
     "yh_reserve": (c_int, [c_void_p, c_int, c_int, c_int]),
     "yh_forward": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p]),
+    "yh_forward_u8": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p]),
     "yh_nms_workspace_bytes": (c_size_t, [c_int, c_int, c_int]),
     "yh_nms": (c_int, [c_int, c_void_p, c_int, c_int, c_int, c_float, c_double, c_int, c_int, c_float,
                        c_void_p, c_size_t, c_void_p, c_void_p, c_void_p]),

@@ -124,11 +124,14 @@ class Engine:
         return a.value
 
     def forward(self, x, out=None):
-        """x: (B, 3, H, W) cuda tensor in the engine dtype -> (B, 4 + nc, A)."""
+        """x: (B, 3, H, W) cuda tensor in the engine dtype -> (B, 4 + nc, A).
+
+        x may also be the loader's uint8 image batch: the reference's `x.half() / 255`
+        (main.py:265-267, to the engine dtype) then runs inside the stem (yh_forward_u8)."""
         if not x.is_cuda or x.device.index != self.index:
             raise ValueError(f"yolo_hip: input must live on cuda:{self.index}")
-        if x.dtype != self.dtype:
-            raise TypeError(f"yolo_hip: input dtype {x.dtype} != engine dtype {self.dtype}")
+        if x.dtype != self.dtype and x.dtype != torch.uint8:
+            raise TypeError(f"yolo_hip: input dtype {x.dtype} is neither the engine dtype {self.dtype} nor uint8")
         if x.dim() != 4 or x.shape[1] != 3:
             raise ValueError(f"yolo_hip: expected (B, 3, H, W), got {tuple(x.shape)}")
         x = x.contiguous()
@@ -136,8 +139,9 @@ class Engine:
         A = self.num_anchors(H, W)
         if out is None:
             out = torch.empty((B, 4 + self.num_classes, A), dtype=self.dtype, device=x.device)
-        check(lib().yh_forward(self._h, c_void_p(x.data_ptr()), B, H, W, c_void_p(out.data_ptr()),
-                               _stream_ptr(x.device)), "forward")
+        fwd = lib().yh_forward_u8 if x.dtype == torch.uint8 else lib().yh_forward
+        check(fwd(self._h, c_void_p(x.data_ptr()), B, H, W, c_void_p(out.data_ptr()), _stream_ptr(x.device)),
+              "forward")
         return out
 
     def reserve(self, batch, height, width):
