@@ -8,6 +8,8 @@
   load_weight           reference utils/util.py:345-355 } yolo_hip.weights: safe checkpoint
   load_ultralytics_weight  utils/util.py:358-516       } reading + key mapping; the HIP
                         engine re-packs the new parameters on the next device forward
+  compute_metric, compute_ap, smooth   utils/util.py:99-120, 225-300, 172-177: the eval
+                        loop's metrics on the device (yolo_hip.metrics)
 
 non_max_suppression semantics: candidate (anchor, class) pairs with score >
 threshold (compared in the tensor dtype), score-descending order with ties
@@ -23,8 +25,10 @@ import random
 import numpy
 import torch
 
+from yolo_hip.metrics import compute_ap, compute_metric, smooth  # noqa: F401
+
 __all__ = ["setup_seed", "wh2xy", "make_anchors", "non_max_suppression", "load_weight",
-           "load_ultralytics_weight"]
+           "load_ultralytics_weight", "compute_metric", "compute_ap", "smooth"]
 
 MAX_WH = 7680
 MAX_DET = 300
