@@ -1113,10 +1113,10 @@ struct Net {
     // captured as a HIP graph, launch units are spread over up to par_streams
     // streams joined by events, so the graph gets the DAG's edges and independent
     // small kernels run side by side instead of back to back.
-    // Opt-in (YH_STREAMS=N): worth ~6 % at v11_n b32 bf16, but hipGraphLaunch of some
-    // multi-branch graphs segfaults inside libamdhip64 (ROCm 7; e.g. fp16 b4 with every
-    // conv forced to conv_stream<4 slots>), so the default keeps one stream.
-    int par_streams = [] { const char* e = getenv("YH_STREAMS"); return e ? std::max(1, std::min(8, atoi(e))) : 1; }();
+    // YH_STREAMS=N (default 6, 1 = one serial chain). A kernel's first launch (which
+    // sets its dynamic-LDS attribute) inside a multi-stream capture made a later
+    // hipGraphLaunch segfault in libamdhip64 (ROCm 7), hence the eager pass before capture.
+    int par_streams = [] { const char* e = getenv("YH_STREAMS"); return e ? std::max(1, std::min(8, atoi(e))) : 6; }();
     std::vector<hipStream_t> aux_streams;
     std::vector<hipEvent_t> unit_events;
     struct Rg { int t, c0, c1; };
@@ -1286,6 +1286,9 @@ struct Net {
         const GraphKey key{B, H, W, in_u8};
         auto it = graphs.find(key);
         if (it == graphs.end()) {
+            // one eager pass first: every kernel of the plan is then loaded and has its
+            // function attributes (dynamic-LDS limits) set outside any stream capture
+            run_ops(B, H, W, s);
             if (!cap_stream) HIPCHECK(hipStreamCreateWithFlags(&cap_stream, hipStreamNonBlocking));
             hipGraph_t g = nullptr;
             HIPCHECK(hipStreamBeginCapture(cap_stream, hipStreamCaptureModeThreadLocal));
