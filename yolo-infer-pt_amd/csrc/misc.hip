@@ -44,10 +44,65 @@ __global__ __launch_bounds__(256) void maxpool5(const T* src, T* dst, int ldc, i
     st_chunk(dst + (long long)m * ldc + cc * 8, f_to_chunk<T>(mx));
 }
 
+// All three pools in one launch: a workgroup owns one (image, 8-channel chunk)
+// plane, staged in LDS once; y1 = mp(x), y2 = mp(y1), y3 = mp(y2) ping-pong
+// between two LDS planes and each is stored to its concat slice. Max is exact,
+// so this is bit-identical to three maxpool5 launches (which it replaces
+// whenever two planes fit in LDS: H * W <= SPPF_MAX_PX).
+constexpr int SPPF_MAX_PX = 4096;
+template <typename T>
+__global__ __launch_bounds__(256) void sppf_fused(const PoolArgs a) {
+    extern __shared__ __attribute__((aligned(16))) uint4 pln[];
+    const int cpp = a.C / 8;
+    const int n = blockIdx.x / cpp, cc = blockIdx.x - n * cpp;
+    const int HW = a.H * a.W;
+    T* img = reinterpret_cast<T*>(a.buf) + (long long)n * HW * a.ldc + cc * 8;
+    uint4* p0 = pln;
+    uint4* p1 = pln + HW;
+    for (int px = threadIdx.x; px < HW; px += 256) p0[px] = *reinterpret_cast<const uint4*>(img + (long long)px * a.ldc);
+    __syncthreads();
+    for (int i = 0; i < 3; ++i) {
+        const uint4* src = (i & 1) ? p1 : p0;
+        uint4* dst = (i & 1) ? p0 : p1;
+        for (int px = threadIdx.x; px < HW; px += 256) {
+            const int h = px / a.W, w = px - h * a.W;
+            float mx[8];
+#pragma unroll
+            for (int e = 0; e < 8; ++e) mx[e] = -INFINITY;
+            for (int hi = max(h - 2, 0); hi <= min(h + 2, a.H - 1); ++hi)
+                for (int wi = max(w - 2, 0); wi <= min(w + 2, a.W - 1); ++wi) {
+                    Chunk<T> c;
+                    c.v[0] = src[hi * a.W + wi];
+                    float f[8];
+                    chunk_to_f(c, f);
+#pragma unroll
+                    for (int e = 0; e < 8; ++e) mx[e] = fmaxf(mx[e], f[e]);
+                }
+            const Chunk<T> o = f_to_chunk<T>(mx);
+            dst[px] = o.v[0];
+            *reinterpret_cast<uint4*>(img + (long long)px * a.ldc + (i + 1) * a.C) = o.v[0];
+        }
+        __syncthreads();
+    }
+}
+
 template <typename T>
 int launch_sppf_t(const PoolArgs& a, hipStream_t s) {
     T* b = reinterpret_cast<T*>(a.buf);
     const int M = a.B * a.H * a.W;
+    if constexpr (sizeof(T) == 2) {
+        if (a.H * a.W <= SPPF_MAX_PX && a.C % 8 == 0) {
+            static bool attr_set = false;
+            if (!attr_set) {
+                (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&sppf_fused<T>),
+                                          hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+                attr_set = true;
+            }
+            hipLaunchKernelGGL((sppf_fused<T>), dim3((unsigned)(a.B * (a.C / 8))), dim3(256),
+                               2 * a.H * a.W * (int)sizeof(uint4), s, a);
+            return (int)hipGetLastError();
+        }
+    }
     const long long n = (long long)M * (a.C / 8);
     const dim3 g((unsigned)((n + 255) / 256));
     for (int i = 0; i < 3; ++i) {
