@@ -1252,50 +1252,83 @@ int launch_first_t(const FirstConvArgs& a, int B, hipStream_t s) {
     return a.in_u8 ? launch_first_tu<T, uint8_t>(a, B, s) : launch_first_tu<T, T>(a, B, s);
 }
 
+// Depthwise 3x3, stride 1, pad 1 (nn.py:248,250). One thread = 8 channels x DW_ROWS
+// vertically adjacent output pixels: the DW_ROWS + 2 input rows it needs are
+// loaded once (no per-tap re-read of the shared rows), all loads are issued before
+// any FMA (branch-free: out-of-image taps read an in-image address and are
+// multiplied by 0, which adds exactly +-0 to a finite sum, so the result equals
+// the skip-the-tap form bit for bit), tap order kh-major as before.
+constexpr int DW_ROWS = 4;
 template <typename T>
 __global__ __launch_bounds__(256) void dwconv3x3(const DwArgs p) {
-    // One thread = one pixel x 8 channels. Stride 1, pad 1 (nn.py:248,250).
     const int cpp = p.C / 8;
-    const long long idx = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-    if (idx >= (long long)p.M * cpp) return;
-    const int m = (int)(idx / cpp), cc = (int)(idx - (long long)m * cpp);
-    const int HW = p.H * p.W;
-    const int n = m / HW, r = m - n * HW;
-    const int h = r / p.W, w = r - h * p.W;
+    const int t = blockIdx.x * 256 + threadIdx.x;
+    if (t >= p.W * cpp) return;
+    const int w = t / cpp, cc = t - w * cpp;
+    const int h0 = blockIdx.y * DW_ROWS, n = blockIdx.z;
     const int c0 = cc * 8;
-    const T* in = reinterpret_cast<const T*>(p.in) + (long long)n * HW * p.ldi + c0;
-    float acc[8];
+    const T* in = reinterpret_cast<const T*>(p.in) + (long long)n * p.H * p.W * p.ldi + c0;
+    float wt[9][8];
 #pragma unroll
-    for (int e = 0; e < 8; ++e) acc[e] = 0.f;
+    for (int k = 0; k < 9; ++k) {
+        const float4 a = *reinterpret_cast<const float4*>(p.w + k * p.C + c0);
+        const float4 b = *reinterpret_cast<const float4*>(p.w + k * p.C + c0 + 4);
+        wt[k][0] = a.x; wt[k][1] = a.y; wt[k][2] = a.z; wt[k][3] = a.w;
+        wt[k][4] = b.x; wt[k][5] = b.y; wt[k][6] = b.z; wt[k][7] = b.w;
+    }
+    Chunk<T> x[DW_ROWS + 2][3];
+    float msk[DW_ROWS + 2][3];
 #pragma unroll
-    for (int kh = 0; kh < 3; ++kh) {
-        const int hi = h - 1 + kh;
-        if (hi < 0 || hi >= p.H) continue;
+    for (int r = 0; r < DW_ROWS + 2; ++r) {
+        const int hi = h0 - 1 + r;
+        const bool hok = (unsigned)hi < (unsigned)p.H;
+        const int hc = min(max(hi, 0), p.H - 1);
 #pragma unroll
         for (int kw = 0; kw < 3; ++kw) {
             const int wi = w - 1 + kw;
-            if (wi < 0 || wi >= p.W) continue;
-            float f[8];
-            chunk_to_f(ld_chunk(in + ((long long)hi * p.W + wi) * p.ldi), f);
-            const float* wt = p.w + (kh * 3 + kw) * p.C + c0;
-#pragma unroll
-            for (int e = 0; e < 8; ++e) acc[e] = fmaf(wt[e], f[e], acc[e]);
+            const bool ok = hok && (unsigned)wi < (unsigned)p.W;
+            const int wc = min(max(wi, 0), p.W - 1);
+            x[r][kw] = ld_chunk(in + ((long long)hc * p.W + wc) * p.ldi);
+            msk[r][kw] = ok ? 1.f : 0.f;
         }
     }
-    float o[8];
+    float bias[8];
 #pragma unroll
-    for (int e = 0; e < 8; ++e) {
-        float v = acc[e] + p.bias[c0 + e];
-        if (p.act == ACT_SILU) v = silu<T>(v);
-        o[e] = v;
+    for (int e = 0; e < 8; ++e) bias[e] = p.bias[c0 + e];
+#pragma unroll
+    for (int o = 0; o < DW_ROWS; ++o) {
+        const int h = h0 + o;
+        if (h >= p.H) break;
+        float acc[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) acc[e] = 0.f;
+#pragma unroll
+        for (int kh = 0; kh < 3; ++kh)
+#pragma unroll
+            for (int kw = 0; kw < 3; ++kw) {
+                float f[8];
+                chunk_to_f(x[o + kh][kw], f);
+                const float mk = msk[o + kh][kw];
+#pragma unroll
+                for (int e = 0; e < 8; ++e) acc[e] = fmaf(wt[kh * 3 + kw][e], f[e] * mk, acc[e]);
+            }
+        float v8[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+            float v = acc[e] + bias[e];
+            if (p.act == ACT_SILU) v = silu<T>(v);
+            v8[e] = v;
+        }
+        const long long m = ((long long)n * p.H + h) * p.W + w;
+        st_chunk(reinterpret_cast<T*>(p.out) + m * p.ldo + c0, f_to_chunk<T>(v8));
     }
-    st_chunk(reinterpret_cast<T*>(p.out) + (long long)m * p.ldo + c0, f_to_chunk<T>(o));
 }
 
 template <typename T>
 int launch_dw_t(const DwArgs& a, hipStream_t s) {
-    const long long n = (long long)a.M * (a.C / 8);
-    hipLaunchKernelGGL((dwconv3x3<T>), dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, a);
+    const int B = a.M / (a.H * a.W);
+    const dim3 g((unsigned)((a.W * (a.C / 8) + 255) / 256), (unsigned)((a.H + DW_ROWS - 1) / DW_ROWS), (unsigned)B);
+    hipLaunchKernelGGL((dwconv3x3<T>), g, dim3(256), 0, s, a);
     return (int)hipGetLastError();
 }
 

@@ -436,13 +436,24 @@ __global__ __launch_bounds__(256) void head_decode(const DecodeArgs p) {
     y[(long long)p.A] = fromf<T>((y1 + y2) / 2.0f * st);
     y[2LL * p.A] = fromf<T>((x2 - x1) * st);
     y[3LL * p.A] = fromf<T>((y2 - y1) * st);
+    // class scores: all chunks of a batch of DEC_CB loaded before any is used (a
+    // load inside the runtime-bound loop would be waited for one round trip at a time)
+    constexpr int DEC_CB = 10;
     const T* cls = src + 64;
-    for (int c = 0; c < p.nc; c += 8) {
-        float f[8];
-        chunk_to_f(ld_chunk(cls + c), f);
+    const int ncc = (p.nc + 7) / 8;
+    for (int c0 = 0; c0 < ncc; c0 += DEC_CB) {
+        Chunk<T> v[DEC_CB];
 #pragma unroll
-        for (int e = 0; e < 8; ++e) {
-            if (c + e < p.nc) y[(long long)(4 + c + e) * p.A] = fromf<T>(1.0f / (1.0f + ex<T>(-f[e])));
+        for (int u = 0; u < DEC_CB; ++u) v[u] = ld_chunk(cls + 8 * min(c0 + u, ncc - 1));
+#pragma unroll
+        for (int u = 0; u < DEC_CB; ++u) {
+            const int c = 8 * (c0 + u);
+            if (c >= p.nc) break;
+            float f[8];
+            chunk_to_f(v[u], f);
+#pragma unroll
+            for (int e = 0; e < 8; ++e)
+                if (c + e < p.nc) y[(long long)(4 + c + e) * p.A] = fromf<T>(1.0f / (1.0f + ex<T>(-f[e])));
         }
     }
 }
