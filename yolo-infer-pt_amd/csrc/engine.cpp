@@ -566,6 +566,13 @@ struct Net {
     int ldc(const View& v) const { return tensors[v.t].C; }
 
     void drop_graphs() {
+        // A graph exec (and the plans / workspace it points into) must not be destroyed
+        // while a replay is still in flight; a multi-branch exec destroyed mid-replay
+        // left libamdhip64 to segfault in a later hipGraphLaunch.
+        if (!graphs.empty() || !plans.empty()) {
+            (void)hipSetDevice(device);
+            (void)hipDeviceSynchronize();
+        }
         for (auto& kv : graphs) (void)hipGraphExecDestroy(kv.second);
         graphs.clear();
         free_plans();
@@ -1113,9 +1120,9 @@ struct Net {
     // captured as a HIP graph, launch units are spread over up to par_streams
     // streams joined by events, so the graph gets the DAG's edges and independent
     // small kernels run side by side instead of back to back.
-    // YH_STREAMS=N (default 6, 1 = one serial chain). A kernel's first launch (which
-    // sets its dynamic-LDS attribute) inside a multi-stream capture made a later
-    // hipGraphLaunch segfault in libamdhip64 (ROCm 7), hence the eager pass before capture.
+    // YH_STREAMS=N (default 6, 1 = one serial chain). Graph execs are only destroyed
+    // once the device is idle (drop_graphs) and every kernel's first launch happens
+    // before capture (forward): both broke later hipGraphLaunch calls otherwise.
     int par_streams = [] { const char* e = getenv("YH_STREAMS"); return e ? std::max(1, std::min(8, atoi(e))) : 6; }();
     std::vector<hipStream_t> aux_streams;
     std::vector<hipEvent_t> unit_events;
