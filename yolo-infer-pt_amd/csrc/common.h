@@ -31,6 +31,8 @@ struct ConvArgs {
     int act;
     int gm, gn;          // tile grid
     const void* zero;    // >= 16 zero bytes in device memory (source of padded taps)
+    int ks;              // > 1: K split over the workgroup's waves (conv_gemm2k), set by
+                         //      the engine's shape rule for 16-bit handles
 };
 
 // First layer: 3-channel NCHW input (the caller's tensor), 3x3 stride-2 conv.

@@ -980,6 +980,226 @@ int launch_direct(const ConvArgs& a, hipStream_t s) {
 #undef YH_DIR
 }
 
+// ---------------------------------------------------------------------------
+// conv_gemm2k: conv_gemm2 (BM 64) with the K walk split over the workgroup's
+// waves, for layers whose few tiles leave CUs idle and whose long K loop is a
+// chain of LDS-DMA round trips (e.g. head.box.2.0: 200 tiles, 36 stages).
+// Wave w = g*KS + z walks K stages z, z+KS, ... for rows g*16*KS .. +16*KS of
+// the tile; the KS stages of one iteration are in flight together. Partial sums
+// meet in LDS and are added in the fixed order z = 0, 1, .., KS-1 - so the
+// result is deterministic, but rounds differently from the single-chain kernels:
+// the engine selects this kernel by a shape rule (ConvArgs::ks), never by timing.
+template <int BN, int KS>
+struct Smem2K {
+    static constexpr int STAGE = 64 * 128 + BN * 128;
+    static constexpr int MAIN = 2 * KS * STAGE;
+    static constexpr int RED = 4 * (BN / 16) * KS * 64 * 16;   // every wave's accumulators
+    static constexpr int EPI = 64 * (BN + 8) * 2;
+    static constexpr int R1 = MAIN > RED ? MAIN : RED;
+    static constexpr int REGION = R1 > EPI ? R1 : EPI;
+};
+
+template <typename T, int BN, int KS>
+__global__ __launch_bounds__(NT_) void conv_gemm2k(const ConvArgs p) {
+    static_assert(sizeof(T) == 2, "16-bit path");
+    constexpr int BM = 64;
+    constexpr int NTL = BN / 16;
+    constexpr int AI = BM / 32;
+    constexpr int MT = KS;          // 16-row MFMA tiles per wave (rows = 16 * KS)
+    using SM = Smem2K<BN, KS>;
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    int* ktab = reinterpret_cast<int*>(smem + SM::REGION);
+
+    const int tid = threadIdx.x;
+    const int lane = tid & 63, wave = tid >> 6;
+    const int z = wave % KS, g = wave / KS;
+    const int lid = xcd_remap(blockIdx.x, p.gm * p.gn);
+    const int mt = lid / p.gn, nt = lid - mt * p.gn;
+    const int m0 = mt * BM, n0 = nt * BN;
+    for (int i = tid; i < p.Kp / 8; i += NT_) ktab[i] = p.ktab[i];
+
+    const int lrow = lane >> 3;
+    const int cidx = (lane & 7) ^ lrow;
+    const int HoWo = p.Ho * p.Wo;
+    int rn[AI], rhb[AI], rwb[AI];
+#pragma unroll
+    for (int i = 0; i < AI; ++i) {
+        const int m = m0 + (wave + 4 * i) * 8 + lrow;
+        if (m < p.M) {
+            const int n = m / HoWo, r = m - n * HoWo;
+            const int ho = r / p.Wo, wo = r - ho * p.Wo;
+            rn[i] = n; rhb[i] = ho * p.stride - p.pad; rwb[i] = wo * p.stride - p.pad;
+        } else {
+            rn[i] = -1; rhb[i] = 0; rwb[i] = 0;
+        }
+    }
+    const T* in0 = reinterpret_cast<const T*>(p.in0);
+    const T* in1 = reinterpret_cast<const T*>(p.in1);
+    const T* wg = reinterpret_cast<const T*>(p.w);
+    const long long bs0 = (long long)p.h0 * p.w0 * p.ldc0;
+    const long long bs1 = (long long)p.h1 * p.w1 * p.ldc1;
+    __syncthreads();  // ktab
+
+    auto issue = [&](int kt, char* a) {
+        char* b = a + BM * 128;
+        const int e = ktab[kt * 8 + cidx];
+        const int kh = e >> 24, kw = (e >> 16) & 0xff, ci = e & 0xffff;
+#pragma unroll
+        for (int i = 0; i < AI; ++i) {
+            const int hi = rhb[i] + kh, wi = rwb[i] + kw;
+            const void* src = p.zero;
+            if (ci != 0xffff && rn[i] >= 0 && hi >= 0 && hi < p.Hi && wi >= 0 && wi < p.Wi) {
+                if (ci < p.c0)
+                    src = in0 + rn[i] * bs0 + ((long long)(hi >> p.up0) * p.w0 + (wi >> p.up0)) * p.ldc0 + ci;
+                else
+                    src = in1 + rn[i] * bs1 + ((long long)(hi >> p.up1) * p.w1 + (wi >> p.up1)) * p.ldc1 + (ci - p.c0);
+            }
+            glds16(src, a + (wave + 4 * i) * 1024);
+        }
+        for (int ii = wave; ii < BN / 8; ii += 4) {
+            const T* src = wg + (long long)(n0 + ii * 8 + lrow) * p.Kp + kt * BK2 + cidx * 8;
+            glds16(src, b + ii * 1024);
+        }
+    };
+    const int nkt = p.Kp / BK2;
+    auto issue_iter = [&](int it, int buf) {
+        for (int zz = 0; zz < KS; ++zz) {
+            const int kt = it * KS + zz;
+            if (kt < nkt) issue(kt, smem + buf * KS * SM::STAGE + zz * SM::STAGE);
+        }
+    };
+
+    f32x4 acc[NTL][MT];
+#pragma unroll
+    for (int i = 0; i < NTL; ++i)
+#pragma unroll
+        for (int j = 0; j < MT; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    const int nit = (nkt + KS - 1) / KS;
+    const int fr = lane & 15, fq = lane >> 4;
+    issue_iter(0, 0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    for (int it = 0; it < nit; ++it) {
+        const int cur = it & 1;
+        if (it + 1 < nit) issue_iter(it + 1, cur ^ 1);
+        if (it * KS + z < nkt) {   // wave-uniform
+            const char* a = smem + cur * KS * SM::STAGE + z * SM::STAGE;
+            const char* b = a + BM * 128;
+#pragma unroll
+            for (int kk = 0; kk < 2; ++kk) {
+                const int chunk = kk * 4 + fq;
+                uint4 wf[NTL];
+#pragma unroll
+                for (int i = 0; i < NTL; ++i) {
+                    const int row = i * 16 + fr;
+                    wf[i] = *reinterpret_cast<const uint4*>(b + row * 128 + ((chunk ^ (row & 7)) << 4));
+                }
+#pragma unroll
+                for (int j = 0; j < MT; ++j) {
+                    const int row = g * (16 * KS) + j * 16 + fr;
+                    const uint4 xa = *reinterpret_cast<const uint4*>(a + row * 128 + ((chunk ^ (row & 7)) << 4));
+#pragma unroll
+                    for (int i = 0; i < NTL; ++i) Mma<T>::step(acc[i][j], &wf[i], &xa);
+                }
+            }
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+    }
+
+    // partials -> LDS, then wave w sums rows w*16 .. w*16+15 over z in order
+    f32x4* red = reinterpret_cast<f32x4*>(smem);
+#pragma unroll
+    for (int i = 0; i < NTL; ++i)
+#pragma unroll
+        for (int j = 0; j < MT; ++j) red[((wave * NTL + i) * MT + j) * 64 + lane] = acc[i][j];
+    __syncthreads();
+    f32x4 sum[NTL];
+    {
+        const int gw = wave / KS, jw = wave % KS;   // (group, tile) holding rows wave*16..
+#pragma unroll
+        for (int i = 0; i < NTL; ++i) {
+            sum[i] = red[(((gw * KS + 0) * NTL + i) * MT + jw) * 64 + lane];
+            for (int zz = 1; zz < KS; ++zz) sum[i] += red[(((gw * KS + zz) * NTL + i) * MT + jw) * 64 + lane];
+        }
+    }
+    __syncthreads();   // the epilogue's staging reuses the reduction area
+
+    constexpr int LDE = BN + 8;
+    T* Cs = reinterpret_cast<T*>(smem);
+#pragma unroll
+    for (int i = 0; i < NTL; ++i) {
+        const int co = i * 16 + fq * 4;
+        float bv[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) bv[r] = p.bias[n0 + co + r];
+        const int px = wave * 16 + fr;
+        T* dst = Cs + px * LDE + co;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            float v = sum[i][r] + bv[r];
+            if (p.act == ACT_SILU) v = silu<T>(v);
+            dst[r] = fromf<T>(v);
+        }
+    }
+    __syncthreads();
+    const T* res = reinterpret_cast<const T*>(p.res);
+    T* out = reinterpret_cast<T*>(p.out);
+    constexpr int CPP = BN / 8;
+    for (int c = tid; c < BM * CPP; c += NT_) {
+        const int px = c / CPP, cc = c - px * CPP;
+        const int m = m0 + px, co = n0 + cc * 8;
+        if (m >= p.M || co >= p.Cout) continue;
+        Chunk<T> v = ld_chunk(Cs + px * LDE + cc * 8);
+        if (res) {
+            float f[8], gg[8];
+            chunk_to_f(v, f);
+            chunk_to_f(ld_chunk(res + (long long)m * p.ldr + co), gg);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) f[e] += gg[e];
+            v = f_to_chunk<T>(f);
+        }
+        st_chunk(out + (long long)m * p.ldo + co, v);
+    }
+}
+
+template <typename T, int BN, int KS>
+int launch_conv2k_t(const ConvArgs& a, hipStream_t s) {
+    using SM = Smem2K<BN, KS>;
+    const int lds = SM::REGION + (a.Kp / 8) * 4;
+    static bool attr_set = false;
+    if (!attr_set) {
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_gemm2k<T, BN, KS>),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        attr_set = true;
+    }
+    ConvArgs b = a;
+    b.gm = (a.M + 63) / 64;
+    b.gn = (a.Cout + BN - 1) / BN;
+    hipLaunchKernelGGL((conv_gemm2k<T, BN, KS>), dim3(b.gm * b.gn), dim3(NT_), lds, s, b);
+    return (int)hipGetLastError();
+}
+
+template <typename T>
+int launch_conv2k(const ConvArgs& a, int BN, hipStream_t s) {
+    if (a.ks == 4) {
+        switch (BN) {
+            case 16: return launch_conv2k_t<T, 16, 4>(a, s);
+            case 32: return launch_conv2k_t<T, 32, 4>(a, s);
+            case 64: return launch_conv2k_t<T, 64, 4>(a, s);
+        }
+    } else if (a.ks == 2) {
+        switch (BN) {
+            case 16: return launch_conv2k_t<T, 16, 2>(a, s);
+            case 32: return launch_conv2k_t<T, 32, 2>(a, s);
+            case 64: return launch_conv2k_t<T, 64, 2>(a, s);
+            case 128: return launch_conv2k_t<T, 128, 2>(a, s);
+        }
+    }
+    return (int)hipErrorInvalidValue;
+}
+
 template <typename T, int BM, int BN>
 int launch_conv2_t(const ConvArgs& a, hipStream_t s) {
     using SM = Smem2<BM, BN>;
@@ -1388,6 +1608,8 @@ bool conv_kernel_ok(int dtype, int kern, const ConvArgs& a) {
 }
 
 int launch_conv(int dtype, int kern, int BM, int BN, const ConvArgs& a, hipStream_t s) {
+    if (dtype != F32 && a.ks > 1)   // shape-ruled K split (deterministic, see conv_gemm2k)
+        return dtype == F16 ? launch_conv2k<_Float16>(a, BN, s) : launch_conv2k<__bf16>(a, BN, s);
     if (!conv_kernel_ok(dtype, kern, a)) return (int)hipErrorInvalidValue;
     if (dtype == F32) return launch_conv_bm<float>(BM, BN, a, s);
     const bool h = dtype == F16;

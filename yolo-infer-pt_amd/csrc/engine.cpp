@@ -147,6 +147,7 @@ struct Net {
     void* zero_dev = nullptr;     // 256 zero bytes: source of padded conv taps
     bool use_graph = true;
     std::map<GraphKey, hipGraphExec_t> graphs;
+    std::map<GraphKey, std::vector<hipEvent_t>> graph_events;   // events a capture used: live as long as its exec
     hipStream_t cap_stream = nullptr;
     bool profile = false;
     std::vector<double> prof_ms;     // per launch unit of the profiled shape
@@ -575,6 +576,9 @@ struct Net {
         }
         for (auto& kv : graphs) (void)hipGraphExecDestroy(kv.second);
         graphs.clear();
+        for (auto& kv : graph_events)
+            for (auto e : kv.second) (void)hipEventDestroy(e);
+        graph_events.clear();
         free_plans();
     }
 
@@ -614,6 +618,20 @@ struct Net {
         a.gm = (a.M + BM - 1) / BM;
         a.gn = (a.Cout + BN - 1) / BN;
         a.zero = zero_dev;
+        a.ks = split_rule(a, BM, BN);
+    }
+    // K split over a workgroup's waves (conv_gemm2k) for 16-bit layers whose BM-64 tiles
+    // number fewer than two per CU and whose K walk is long: a fixed shape rule (the
+    // split rounds differently from the single-chain kernels, so it is never a timing
+    // choice); YH_KSPLIT=0 turns it off.
+    int split_rule(const ConvArgs& a, int BM, int BN) const {
+        static const bool on = [] { const char* e = getenv("YH_KSPLIT"); return !e || atoi(e) != 0; }();
+        if (!on || dtype == F32 || BM != 64 || BN > 128) return 1;
+        const int tiles = a.gm * a.gn, nkt = a.Kp / 64;
+        // measured (r01): 4 slices pay off only for the long walks (head.box.2.0, K = 2304:
+        // 46 -> 33 us); 2 slices on K <= 1152 layers were 10-40 % slower, so they stay off
+        if (tiles >= 512 || nkt < 16 || BN > 64) return 1;
+        return 4;
     }
 
     DwArgs dw_args(const Op& op, int B, int H, int W) const {
@@ -677,7 +695,7 @@ struct Net {
                     for (auto& u : cur_plan->units)
                         if (u.level) for (int k = u.first; k < u.last; ++k) fused[k] = 1;
                 for (size_t i = 0; i < ops.size(); ++i) {
-                    if (ops[i].kind != OP_CONV || fused[i]) continue;
+                    if (ops[i].kind != OP_CONV || fused[i] || args[i].ks > 1) continue;   // ks: fixed by rule
                     float best = 1e30f;
                     for (int k = 0; k < CONV_NKERNELS; ++k) {
                         if (!conv_kernel_ok(dtype, k, args[i])) continue;
@@ -1120,10 +1138,13 @@ struct Net {
     // captured as a HIP graph, launch units are spread over up to par_streams
     // streams joined by events, so the graph gets the DAG's edges and independent
     // small kernels run side by side instead of back to back.
-    // YH_STREAMS=N (default 6, 1 = one serial chain). Graph execs are only destroyed
-    // once the device is idle (drop_graphs) and every kernel's first launch happens
-    // before capture (forward): both broke later hipGraphLaunch calls otherwise.
-    int par_streams = [] { const char* e = getenv("YH_STREAMS"); return e ? std::max(1, std::min(8, atoi(e))) : 6; }();
+    // YH_STREAMS=N (opt-in; default 1 = one serial chain). Worth ~8 % at v11_n b32 bf16
+    // (1.65 vs 1.79 ms per step), but hipGraphLaunch of these multi-branch graphs still
+    // segfaults intermittently inside libamdhip64 (ROCm 7.2) when graphs are re-captured
+    // (tests/test_gpu_conv_kernels.py), even with the mitigations kept here: graph execs
+    // destroyed only on an idle device, fork/join events kept alive with their exec, and
+    // every kernel's first launch made before capture.
+    int par_streams = [] { const char* e = getenv("YH_STREAMS"); return e ? std::max(1, std::min(8, atoi(e))) : 1; }();
     std::vector<hipStream_t> aux_streams;
     std::vector<hipEvent_t> unit_events;
     struct Rg { int t, c0, c1; };
@@ -1157,9 +1178,8 @@ struct Net {
             HIPCHECK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
             aux_streams.push_back(st);
         }
-        // fresh events per capture: HIP keeps a reference to the capture node an event
-        // was recorded at, so reusing one in a later capture (after that graph was
-        // destroyed) dereferences a dead node. forward() destroys them after EndCapture.
+        // fresh events per capture, never reused: forward() hands them to the graph
+        // exec they were captured into, and drop_graphs destroys them with it.
         release_unit_events();
         for (int i = 0; i < n + NS; ++i) {
             hipEvent_t e;
@@ -1310,13 +1330,16 @@ struct Net {
             }
             if (bt) fprintf(stderr, "[yh] captured B=%d H=%d W=%d streams=%d\n", B, H, W, par_streams);
             HIPCHECK(hipStreamEndCapture(cap_stream, &g));
-            release_unit_events();
             if (bt) fprintf(stderr, "[yh] capture ended\n");
             hipGraphExec_t ex = nullptr;
             HIPCHECK(hipGraphInstantiate(&ex, g, nullptr, nullptr, 0));
             if (bt) fprintf(stderr, "[yh] instantiated\n");
             (void)hipGraphDestroy(g);
             it = graphs.emplace(key, ex).first;
+            // the capture's fork/join events stay alive with the exec (destroying them
+            // right after capture left a later hipGraphLaunch to segfault intermittently)
+            graph_events[key] = std::move(unit_events);
+            unit_events.clear();
         }
         HIPCHECK(hipGraphLaunch(it->second, s));
     }
@@ -1718,6 +1741,13 @@ int yh_op_kernel(const yh_handle* h, int index, int batch, int height, int width
         }
         auto it = n.conv_kern.find(yh::GraphKey{batch, height, width});
         yh::require(it != n.conv_kern.end(), "no forward has run at this shape yet", YH_ESTATE);
+        yh::ConvArgs a{};
+        int BM = 0, BN = 0;
+        n.conv_args(op, batch, height, width, a, BM, BN);
+        if (a.ks > 1) {
+            if (name) *name = a.ks == 4 ? "ksplit4" : "ksplit2";
+            return;
+        }
         if (name) *name = conv_names[it->second[index]];
     });
 }
