@@ -1255,6 +1255,96 @@ struct Net {
         }
     }
 
+    // ---------------------------------------------------------- head split
+    // The detect head's box branches (head.box.*) and class branches (head.cls.*)
+    // are independent: they read the FPN outputs and write disjoint channel slices
+    // of the per-level head tensors; only the decode joins them. The forward is
+    // replayed as four single-chain graphs - A (backbone + FPN) and C (class
+    // branches) on the caller's stream, B (box branches) on a second stream after
+    // A, D (decode) after both - so the two branches overlap. Single-chain graphs
+    // joined by events between launches avoid HIP's multi-branch graph executor
+    // (see par_streams). YH_HEADSPLIT=0 turns it off.
+    bool head_split = [] { const char* e = getenv("YH_HEADSPLIT"); return !e || atoi(e) != 0; }();
+    hipStream_t hs_stream = nullptr;
+    hipEvent_t hs_ev[2] = {nullptr, nullptr};
+    // segment of each unit (0 A, 1 B, 2 C, 3 D) if the plan splits cleanly, else empty
+    std::vector<int> head_segments() const {
+        const auto& us = cur_plan->units;
+        const int n = (int)us.size();
+        std::vector<int> seg(n, 0);
+        int first_head = n;
+        for (int j = 0; j < n; ++j) {
+            const Unit& u = us[j];
+            const std::string& lb = ops[u.first].label;
+            const bool box = lb.rfind("head.box.", 0) == 0, cls = lb.rfind("head.cls.", 0) == 0;
+            const bool dec = ops[u.first].kind == OP_DECODE;
+            if (u.level && (box || cls || dec)) return {};   // a fused level unit spans segments
+            seg[j] = box ? 1 : cls ? 2 : dec ? 3 : 0;
+            if (seg[j] && first_head == n) first_head = j;
+            if (!seg[j] && j > first_head) return {};        // backbone / FPN work after the head
+        }
+        if (first_head == n || seg[n - 1] != 3) return {};
+        for (int j = 0; j < n - 1; ++j)
+            if (seg[j] == 3) return {};
+        // box and class units must not touch the same channels
+        std::vector<std::vector<Rg>> rd(n), wr(n);
+        for (int j = first_head; j < n; ++j) unit_regions(us[j], rd[j], wr[j]);
+        auto ov = [](const std::vector<Rg>& a, const std::vector<Rg>& b) {
+            for (auto& x : a)
+                for (auto& y : b)
+                    if (x.t == y.t && x.c0 < y.c1 && y.c0 < x.c1) return true;
+            return false;
+        };
+        for (int i = first_head; i < n; ++i)
+            for (int j = first_head; j < n; ++j)
+                if (seg[i] == 1 && seg[j] == 2 && (ov(wr[i], rd[j]) || ov(rd[i], wr[j]) || ov(wr[i], wr[j])))
+                    return {};
+        return seg;
+    }
+    hipGraphExec_t capture_segment(const std::vector<int>& seg, int which, int B, int H, int W) {
+        if (!cap_stream) HIPCHECK(hipStreamCreateWithFlags(&cap_stream, hipStreamNonBlocking));
+        hipGraph_t g = nullptr;
+        HIPCHECK(hipStreamBeginCapture(cap_stream, hipStreamCaptureModeThreadLocal));
+        try {
+            for (size_t j = 0; j < seg.size(); ++j)
+                if (seg[j] == which) launch_unit(cur_plan->units[j], B, H, W, cap_stream);
+        } catch (...) {
+            (void)hipStreamEndCapture(cap_stream, &g);
+            if (g) (void)hipGraphDestroy(g);
+            throw;
+        }
+        HIPCHECK(hipStreamEndCapture(cap_stream, &g));
+        hipGraphExec_t ex = nullptr;
+        HIPCHECK(hipGraphInstantiate(&ex, g, nullptr, nullptr, 0));
+        (void)hipGraphDestroy(g);
+        return ex;
+    }
+    // true if the forward was launched as the four head-split graphs
+    bool forward_head_split(int B, int H, int W, hipStream_t s) {
+        GraphKey k0{B, H, W, in_u8 | 2};
+        auto it = graphs.find(k0);
+        if (it == graphs.end()) {
+            const std::vector<int> seg = head_segments();
+            if (seg.empty()) return false;
+            run_ops(B, H, W, s);   // eager pass: first launches outside any capture
+            for (int w = 0; w < 4; ++w)
+                graphs.emplace(GraphKey{B, H, W, in_u8 | ((w + 1) << 1)}, capture_segment(seg, w, B, H, W));
+            if (!hs_stream) HIPCHECK(hipStreamCreateWithFlags(&hs_stream, hipStreamNonBlocking));
+            for (auto& e : hs_ev)
+                if (!e) HIPCHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+        }
+        auto g = [&](int w) { return graphs.at(GraphKey{B, H, W, in_u8 | ((w + 1) << 1)}); };
+        HIPCHECK(hipGraphLaunch(g(0), s));              // A: backbone + FPN
+        HIPCHECK(hipEventRecord(hs_ev[0], s));
+        HIPCHECK(hipStreamWaitEvent(hs_stream, hs_ev[0], 0));
+        HIPCHECK(hipGraphLaunch(g(1), hs_stream));      // B: box branches, beside C
+        HIPCHECK(hipEventRecord(hs_ev[1], hs_stream));
+        HIPCHECK(hipGraphLaunch(g(2), s));              // C: class branches
+        HIPCHECK(hipStreamWaitEvent(s, hs_ev[1], 0));
+        HIPCHECK(hipGraphLaunch(g(3), s));              // D: decode
+        return true;
+    }
+
     void run_ops(int B, int H, int W, hipStream_t s) {
         if (!cur_plan) {
             for (size_t i = 0; i < ops.size(); ++i) launch_op(i, B, H, W, s);
@@ -1310,6 +1400,7 @@ struct Net {
             run_ops(B, H, W, s);
             return;
         }
+        if (head_split && par_streams == 1 && forward_head_split(B, H, W, s)) return;
         const GraphKey key{B, H, W, in_u8};
         auto it = graphs.find(key);
         if (it == graphs.end()) {
@@ -1425,6 +1516,9 @@ struct Net {
         if (zero_dev) (void)hipFree(zero_dev);
         if (cap_stream) (void)hipStreamDestroy(cap_stream);
         for (auto st : aux_streams) (void)hipStreamDestroy(st);
+        if (hs_stream) (void)hipStreamDestroy(hs_stream);
+        for (auto e : hs_ev)
+            if (e) (void)hipEventDestroy(e);
         release_unit_events();
         for (auto e : ev) (void)hipEventDestroy(e);
     }
