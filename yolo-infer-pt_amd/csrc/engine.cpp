@@ -1255,15 +1255,16 @@ struct Net {
         }
     }
 
-    // ---------------------------------------------------------- head split
-    // The detect head's box branches (head.box.*) and class branches (head.cls.*)
-    // are independent: they read the FPN outputs and write disjoint channel slices
-    // of the per-level head tensors; only the decode joins them. The forward is
-    // replayed as four single-chain graphs - A (backbone + FPN) and C (class
-    // branches) on the caller's stream, B (box branches) on a second stream after
-    // A, D (decode) after both - so the two branches overlap. Single-chain graphs
-    // joined by events between launches avoid HIP's multi-branch graph executor
-    // (see par_streams). YH_HEADSPLIT=0 turns it off.
+    // ---------------------------------------------------------- segment split
+    // The forward is replayed as four single-chain graphs on two streams, joined by
+    // events between launches (no multi-branch graph: see par_streams):
+    //   A  backbone + FPN top-down (through fpn.h2, which produces P3')   stream 0
+    //   B  the 80x80 detect head (head.box.0.*, head.cls.0.*)             stream 1, after A
+    //   C  FPN bottom-up (fpn.h3 ..) + the 40x40 / 20x20 heads           stream 0
+    //   D  decode                                                         stream 0, after B
+    // B is throughput work (the largest head level) and C is a chain of small,
+    // latency-bound layers, so B fills the CUs C leaves idle. The split is checked
+    // against the channel-range dependencies of every unit. YH_HEADSPLIT=0 turns it off.
     bool head_split = [] { const char* e = getenv("YH_HEADSPLIT"); return !e || atoi(e) != 0; }();
     hipStream_t hs_stream = nullptr;
     hipEvent_t hs_ev[2] = {nullptr, nullptr};
@@ -1272,33 +1273,41 @@ struct Net {
         const auto& us = cur_plan->units;
         const int n = (int)us.size();
         std::vector<int> seg(n, 0);
-        int first_head = n;
+        int last_a = -1;
         for (int j = 0; j < n; ++j) {
             const Unit& u = us[j];
             const std::string& lb = ops[u.first].label;
-            const bool box = lb.rfind("head.box.", 0) == 0, cls = lb.rfind("head.cls.", 0) == 0;
+            const bool h0 = lb.rfind("head.box.0.", 0) == 0 || lb.rfind("head.cls.0.", 0) == 0;
             const bool dec = ops[u.first].kind == OP_DECODE;
-            if (u.level && (box || cls || dec)) return {};   // a fused level unit spans segments
-            seg[j] = box ? 1 : cls ? 2 : dec ? 3 : 0;
-            if (seg[j] && first_head == n) first_head = j;
-            if (!seg[j] && j > first_head) return {};        // backbone / FPN work after the head
+            if (u.level && (h0 || dec)) return {};   // a fused level unit spans segments
+            for (int k = u.first; k < u.last; ++k)
+                if (ops[k].label.rfind("fpn.h2", 0) == 0) last_a = j;
+            seg[j] = h0 ? 1 : dec ? 3 : 0;
         }
-        if (first_head == n || seg[n - 1] != 3) return {};
+        if (last_a < 0 || seg[n - 1] != 3) return {};
+        for (int j = last_a + 1; j < n; ++j)
+            if (seg[j] == 0) seg[j] = 2;
+        for (int j = 0; j <= last_a; ++j)
+            if (seg[j] != 0) return {};               // head work before the split point
         for (int j = 0; j < n - 1; ++j)
             if (seg[j] == 3) return {};
-        // box and class units must not touch the same channels
+        // every dependency must run forward along the segment order A -> {B, C} -> D,
+        // and nothing may link B and C
         std::vector<std::vector<Rg>> rd(n), wr(n);
-        for (int j = first_head; j < n; ++j) unit_regions(us[j], rd[j], wr[j]);
+        for (int j = 0; j < n; ++j) unit_regions(us[j], rd[j], wr[j]);
         auto ov = [](const std::vector<Rg>& a, const std::vector<Rg>& b) {
             for (auto& x : a)
                 for (auto& y : b)
                     if (x.t == y.t && x.c0 < y.c1 && y.c0 < x.c1) return true;
             return false;
         };
-        for (int i = first_head; i < n; ++i)
-            for (int j = first_head; j < n; ++j)
-                if (seg[i] == 1 && seg[j] == 2 && (ov(wr[i], rd[j]) || ov(rd[i], wr[j]) || ov(wr[i], wr[j])))
-                    return {};
+        for (int j = 0; j < n; ++j)
+            for (int i = 0; i < j; ++i) {
+                if (!(ov(wr[i], rd[j]) || ov(rd[i], wr[j]) || ov(wr[i], wr[j]))) continue;
+                const int si = seg[i], sj = seg[j];
+                const bool ok = si == sj || si == 0 || sj == 3;
+                if (!ok) return {};
+            }
         return seg;
     }
     hipGraphExec_t capture_segment(const std::vector<int>& seg, int which, int B, int H, int W) {
@@ -1334,12 +1343,12 @@ struct Net {
                 if (!e) HIPCHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
         }
         auto g = [&](int w) { return graphs.at(GraphKey{B, H, W, in_u8 | ((w + 1) << 1)}); };
-        HIPCHECK(hipGraphLaunch(g(0), s));              // A: backbone + FPN
+        HIPCHECK(hipGraphLaunch(g(0), s));              // A: backbone + FPN top-down
         HIPCHECK(hipEventRecord(hs_ev[0], s));
         HIPCHECK(hipStreamWaitEvent(hs_stream, hs_ev[0], 0));
-        HIPCHECK(hipGraphLaunch(g(1), hs_stream));      // B: box branches, beside C
+        HIPCHECK(hipGraphLaunch(g(1), hs_stream));      // B: 80x80 head, beside C
         HIPCHECK(hipEventRecord(hs_ev[1], hs_stream));
-        HIPCHECK(hipGraphLaunch(g(2), s));              // C: class branches
+        HIPCHECK(hipGraphLaunch(g(2), s));              // C: FPN bottom-up + small heads
         HIPCHECK(hipStreamWaitEvent(s, hs_ev[1], 0));
         HIPCHECK(hipGraphLaunch(g(3), s));              // D: decode
         return true;
