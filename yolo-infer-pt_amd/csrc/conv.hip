@@ -12,6 +12,7 @@
 // the BN folded into conv' (fuse_conv, nets/nn.py:8-25); Residual (nn.py:48-49)
 // = x + act(conv'(...)) -> residual added after the activation.
 #include <cstdlib>
+#include <type_traits>
 
 #include "common.h"
 #include "dtypes.h"
@@ -1297,33 +1298,56 @@ __device__ __forceinline__ void stem_in8(const U* p, float (&f)[8]) {
     }
 }
 
+// Stage the block's input window (3 channels x 3 rows x STEM_SEG columns) into the
+// float LDS patch. W is a multiple of 8 and the window is 8-aligned, so each
+// 8-element chunk is wholly inside the image or wholly padding: every load is
+// issued before any is used (clamped address + select, no branch), one round trip.
+constexpr int STEM_CPS = STEM_SEG / 8;
+constexpr int STEM_NCH = (9 * STEM_CPS + STEM_TW - 1) / STEM_TW;
+template <typename T, typename U>
+__device__ __forceinline__ void stem_stage(const U* x, const FirstConvArgs& p, int n, int ho, int col0,
+                                           float (*patch)[STEM_SEG]) {
+    const long long plane = (long long)p.H * p.W;
+    using Raw = typename std::conditional<sizeof(U) == 1, uint2, Chunk<U>>::type;   // 8 elements
+    Raw raw[STEM_NCH];
+    bool ok[STEM_NCH];
+    int dst[STEM_NCH];
+#pragma unroll
+    for (int u = 0; u < STEM_NCH; ++u) {
+        const int c = min((int)threadIdx.x + u * STEM_TW, 9 * STEM_CPS - 1);   // past the end: redo the last
+        const int seg = c / STEM_CPS, ch = c - seg * STEM_CPS;
+        const int ci = seg / 3, kh = seg - ci * 3;
+        const int hi = 2 * ho - 1 + kh;
+        const int col = col0 + ch * 8;
+        ok[u] = hi >= 0 && hi < p.H && col >= 0 && col + 8 <= p.W;
+        const int hc = min(max(hi, 0), p.H - 1), cc = min(max(col, 0), p.W - 8);
+        raw[u] = *reinterpret_cast<const Raw*>(x + ((long long)n * 3 + ci) * plane + (long long)hc * p.W + cc);
+        dst[u] = c;
+    }
+#pragma unroll
+    for (int u = 0; u < STEM_NCH; ++u) {
+        float f[8];
+        if constexpr (sizeof(U) == 1) {
+#pragma unroll
+            for (int e = 0; e < 8; ++e)
+                f[e] = stem_in<uint8_t, T>((uint8_t)((((const uint2&)raw[u]).x >> (8 * (e & 3)) & 255u) * (e < 4) +
+                                                     (((const uint2&)raw[u]).y >> (8 * (e & 3)) & 255u) * (e >= 4)));
+        } else {
+            chunk_to_f(raw[u], f);
+        }
+        const int seg = dst[u] / STEM_CPS, ch = dst[u] - seg * STEM_CPS;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) patch[seg][ch * 8 + e] = ok[u] ? f[e] : 0.f;
+    }
+}
+
 template <typename T, typename U, int NC8>
 __global__ __launch_bounds__(STEM_TW) void conv_first(const FirstConvArgs p) {
     __shared__ float patch[9][STEM_SEG];
     const int wo0 = blockIdx.x * STEM_TW, ho = blockIdx.y, n = blockIdx.z;
     const U* x = reinterpret_cast<const U*>(p.io[0]);
-    const long long plane = (long long)p.H * p.W;
     const int col0 = 2 * wo0 - 8;  // 16-B aligned window start (8 elements before the first tap)
-    constexpr int CPS = STEM_SEG / 8;
-    for (int c = threadIdx.x; c < 9 * CPS; c += STEM_TW) {
-        const int seg = c / CPS, ch = c - seg * CPS;
-        const int ci = seg / 3, kh = seg - ci * 3;
-        const int hi = 2 * ho - 1 + kh;
-        const int col = col0 + ch * 8;
-        float f[8];
-        if (hi >= 0 && hi < p.H && col >= 0 && col + 8 <= p.W) {
-            stem_in8<U, T>(x + ((long long)n * 3 + ci) * plane + (long long)hi * p.W + col, f);
-        } else {
-#pragma unroll
-            for (int e = 0; e < 8; ++e) {
-                const int cc = col + e;
-                f[e] = (hi >= 0 && hi < p.H && cc >= 0 && cc < p.W)
-                           ? stem_in<U, T>(x[((long long)n * 3 + ci) * plane + (long long)hi * p.W + cc]) : 0.f;
-            }
-        }
-#pragma unroll
-        for (int e = 0; e < 8; ++e) patch[seg][ch * 8 + e] = f[e];
-    }
+    stem_stage<T, U>(x, p, n, ho, col0, patch);
     __syncthreads();
     const int wo = wo0 + threadIdx.x;
     const bool live = wo < p.Wo;  // no early exit: keep the weight loads wave-uniform (scalar)
@@ -1363,28 +1387,8 @@ __global__ __launch_bounds__(STEM_TW) void conv_first_mfma(const FirstConvArgs p
     __shared__ float patch[9][STEM_SEG];
     const int wo0 = blockIdx.x * STEM_TW, ho = blockIdx.y, n = blockIdx.z;
     const U* x = reinterpret_cast<const U*>(p.io[0]);
-    const long long plane = (long long)p.H * p.W;
     const int col0 = 2 * wo0 - 8;
-    constexpr int CPS = STEM_SEG / 8;
-    for (int c = threadIdx.x; c < 9 * CPS; c += STEM_TW) {
-        const int seg = c / CPS, ch = c - seg * CPS;
-        const int ci = seg / 3, kh = seg - ci * 3;
-        const int hi = 2 * ho - 1 + kh;
-        const int col = col0 + ch * 8;
-        float f[8];
-        if (hi >= 0 && hi < p.H && col >= 0 && col + 8 <= p.W) {
-            stem_in8<U, T>(x + ((long long)n * 3 + ci) * plane + (long long)hi * p.W + col, f);
-        } else {
-#pragma unroll
-            for (int e = 0; e < 8; ++e) {
-                const int cc = col + e;
-                f[e] = (hi >= 0 && hi < p.H && cc >= 0 && cc < p.W)
-                           ? stem_in<U, T>(x[((long long)n * 3 + ci) * plane + (long long)hi * p.W + cc]) : 0.f;
-            }
-        }
-#pragma unroll
-        for (int e = 0; e < 8; ++e) patch[seg][ch * 8 + e] = f[e];
-    }
+    stem_stage<T, U>(x, p, n, ho, col0, patch);
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int fr = lane & 15, g = lane >> 4;
     // A fragments: weights[cout = 16i + fr][k = 8g + j]
