@@ -14,6 +14,11 @@ namespace {
 
 template <typename T> __device__ __forceinline__ float ex(float x) { return __expf(x); }
 template <> __device__ __forceinline__ float ex<float>(float x) { return expf(x); }
+// a / b: correctly rounded on the f32 (parity) path, hardware reciprocal on the
+// 16-bit paths, whose outputs are rounded to 8 / 11 mantissa bits anyway (same
+// policy as silu, dtypes.h)
+template <typename T> __device__ __forceinline__ float dv(float a, float b) { return a * __builtin_amdgcn_rcpf(b); }
+template <> __device__ __forceinline__ float dv<float>(float a, float b) { return a / b; }
 
 template <typename T>
 __global__ __launch_bounds__(256) void maxpool5(const T* src, T* dst, int ldc, int C, int H, int W, int M) {
@@ -425,7 +430,7 @@ __global__ __launch_bounds__(256) void head_decode(const DecodeArgs p) {
         for (int i = 0; i < 16; ++i) { v[i] = ex<T>(v[i] - mx); sum += v[i]; }
         float d = 0.f;
 #pragma unroll
-        for (int i = 0; i < 16; ++i) d = fmaf((float)i, v[i] / sum, d);
+        for (int i = 0; i < 16; ++i) d = fmaf((float)i, dv<T>(v[i], sum), d);
         dist[sd] = d;
     }
     const float ax = (float)gx + 0.5f, ay = (float)gy + 0.5f, st = p.stride[l];
@@ -453,7 +458,7 @@ __global__ __launch_bounds__(256) void head_decode(const DecodeArgs p) {
             chunk_to_f(v[u], f);
 #pragma unroll
             for (int e = 0; e < 8; ++e)
-                if (c + e < p.nc) y[(long long)(4 + c + e) * p.A] = fromf<T>(1.0f / (1.0f + ex<T>(-f[e])));
+                if (c + e < p.nc) y[(long long)(4 + c + e) * p.A] = fromf<T>(dv<T>(1.0f, 1.0f + ex<T>(-f[e])));
         }
     }
 }
