@@ -398,75 +398,110 @@ int launch_attention_t(const AttnArgs& a, int B, hipStream_t s) {
     return (int)hipGetLastError();
 }
 
-template <typename T>
+// One workgroup = 256 consecutive anchors of one image. Each thread decodes its
+// anchor into a column of an LDS tile [4 + nc][256]; the tile then leaves as
+// 16-B (fp32: 32-B) row chunks of the channel-major output instead of 4 + nc
+// scalar stores per thread. Needs A % 8 == 0 (aligned row chunks); otherwise
+// every value is stored directly (ROWS = false).
+template <typename T, bool ROWS>
 __global__ __launch_bounds__(256) void head_decode(const DecodeArgs p) {
-    const long long idx = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-    if (idx >= (long long)p.B * p.A) return;
-    const int n = (int)(idx / p.A), a = (int)(idx - (long long)n * p.A);
-    int l = 0, loc = a;
-    const int a0 = p.H[0] * p.W[0], a1 = p.H[1] * p.W[1];
-    if (loc >= a0) { loc -= a0; l = 1; if (loc >= a1) { loc -= a1; l = 2; } }
-    const int H = p.H[l], W = p.W[l];
-    const int gy = loc / W, gx = loc - gy * W;
-    const T* src = reinterpret_cast<const T*>(p.lvl[l]) + ((long long)n * H * W + loc) * p.ldc;
+    extern __shared__ __attribute__((aligned(16))) char dsm[];
+    T* tile = reinterpret_cast<T*>(dsm);              // [(4 + nc)][256]
+    const int n = blockIdx.y, a0 = blockIdx.x * 256;
+    const int a = a0 + threadIdx.x;
+    const bool live = a < p.A;
+    T* yimg = reinterpret_cast<T*>(const_cast<void*>(p.io[1])) + (long long)n * (4 + p.nc) * p.A;
+    auto put = [&](int r, float v) {
+        if constexpr (ROWS) tile[r * 256 + threadIdx.x] = fromf<T>(v);
+        else if (live) yimg[(long long)r * p.A + a] = fromf<T>(v);
+    };
+    {
+        const int aa = live ? a : p.A - 1;   // dead lanes decode a valid anchor that is never stored
+        int l = 0, loc = aa;
+        const int l0 = p.H[0] * p.W[0], l1 = p.H[1] * p.W[1];
+        if (loc >= l0) { loc -= l0; l = 1; if (loc >= l1) { loc -= l1; l = 2; } }
+        const int H = p.H[l], W = p.W[l];
+        const int gy = loc / W, gx = loc - gy * W;
+        const T* src = reinterpret_cast<const T*>(p.lvl[l]) + ((long long)n * H * W + loc) * p.ldc;
 
-    // DFL: softmax over 16 bins per side, expectation with weights 0..15.
-    float dist[4];
+        // DFL: softmax over 16 bins per side, expectation with weights 0..15.
+        float dist[4];
 #pragma unroll
-    for (int sd = 0; sd < 4; ++sd) {
-        float v[16];
+        for (int sd = 0; sd < 4; ++sd) {
+            float v[16];
 #pragma unroll
-        for (int c = 0; c < 16; c += 8) {
-            float f[8];
-            chunk_to_f(ld_chunk(src + sd * 16 + c), f);
+            for (int c = 0; c < 16; c += 8) {
+                float f[8];
+                chunk_to_f(ld_chunk(src + sd * 16 + c), f);
 #pragma unroll
-            for (int e = 0; e < 8; ++e) v[c + e] = f[e];
+                for (int e = 0; e < 8; ++e) v[c + e] = f[e];
+            }
+            float mx = v[0];
+#pragma unroll
+            for (int i = 1; i < 16; ++i) mx = fmaxf(mx, v[i]);
+            float sum = 0.f;
+#pragma unroll
+            for (int i = 0; i < 16; ++i) { v[i] = ex<T>(v[i] - mx); sum += v[i]; }
+            float d = 0.f;
+#pragma unroll
+            for (int i = 0; i < 16; ++i) d = fmaf((float)i, dv<T>(v[i], sum), d);
+            dist[sd] = d;
         }
-        float mx = v[0];
+        const float ax = (float)gx + 0.5f, ay = (float)gy + 0.5f, st = p.stride[l];
+        const float x1 = ax - dist[0], y1 = ay - dist[1];
+        const float x2 = ax + dist[2], y2 = ay + dist[3];
+        put(0, (x1 + x2) / 2.0f * st);
+        put(1, (y1 + y2) / 2.0f * st);
+        put(2, (x2 - x1) * st);
+        put(3, (y2 - y1) * st);
+        // class scores: all chunks of a batch of DEC_CB loaded before any is used (a
+        // load inside the runtime-bound loop would be waited for one round trip at a time)
+        constexpr int DEC_CB = 10;
+        const T* cls = src + 64;
+        const int ncc = (p.nc + 7) / 8;
+        for (int c0 = 0; c0 < ncc; c0 += DEC_CB) {
+            Chunk<T> v[DEC_CB];
 #pragma unroll
-        for (int i = 1; i < 16; ++i) mx = fmaxf(mx, v[i]);
-        float sum = 0.f;
+            for (int u = 0; u < DEC_CB; ++u) v[u] = ld_chunk(cls + 8 * min(c0 + u, ncc - 1));
 #pragma unroll
-        for (int i = 0; i < 16; ++i) { v[i] = ex<T>(v[i] - mx); sum += v[i]; }
-        float d = 0.f;
+            for (int u = 0; u < DEC_CB; ++u) {
+                const int c = 8 * (c0 + u);
+                if (c >= p.nc) break;
+                float f[8];
+                chunk_to_f(v[u], f);
 #pragma unroll
-        for (int i = 0; i < 16; ++i) d = fmaf((float)i, dv<T>(v[i], sum), d);
-        dist[sd] = d;
+                for (int e = 0; e < 8; ++e)
+                    if (c + e < p.nc) put(4 + c + e, dv<T>(1.0f, 1.0f + ex<T>(-f[e])));
+            }
+        }
     }
-    const float ax = (float)gx + 0.5f, ay = (float)gy + 0.5f, st = p.stride[l];
-    const float x1 = ax - dist[0], y1 = ay - dist[1];
-    const float x2 = ax + dist[2], y2 = ay + dist[3];
-    T* y = reinterpret_cast<T*>(const_cast<void*>(p.io[1])) + (long long)n * (4 + p.nc) * p.A + a;
-    y[0] = fromf<T>((x1 + x2) / 2.0f * st);
-    y[(long long)p.A] = fromf<T>((y1 + y2) / 2.0f * st);
-    y[2LL * p.A] = fromf<T>((x2 - x1) * st);
-    y[3LL * p.A] = fromf<T>((y2 - y1) * st);
-    // class scores: all chunks of a batch of DEC_CB loaded before any is used (a
-    // load inside the runtime-bound loop would be waited for one round trip at a time)
-    constexpr int DEC_CB = 10;
-    const T* cls = src + 64;
-    const int ncc = (p.nc + 7) / 8;
-    for (int c0 = 0; c0 < ncc; c0 += DEC_CB) {
-        Chunk<T> v[DEC_CB];
-#pragma unroll
-        for (int u = 0; u < DEC_CB; ++u) v[u] = ld_chunk(cls + 8 * min(c0 + u, ncc - 1));
-#pragma unroll
-        for (int u = 0; u < DEC_CB; ++u) {
-            const int c = 8 * (c0 + u);
-            if (c >= p.nc) break;
-            float f[8];
-            chunk_to_f(v[u], f);
-#pragma unroll
-            for (int e = 0; e < 8; ++e)
-                if (c + e < p.nc) y[(long long)(4 + c + e) * p.A] = fromf<T>(dv<T>(1.0f, 1.0f + ex<T>(-f[e])));
+    if constexpr (ROWS) {
+        __syncthreads();
+        const int rows = 4 + p.nc;
+        for (int c = threadIdx.x; c < rows * 32; c += 256) {
+            const int r = c >> 5, k = c & 31;
+            const int a8 = a0 + 8 * k;
+            if (a8 >= p.A) continue;
+            const T* srow = tile + r * 256 + 8 * k;
+            T* drow = yimg + (long long)r * p.A + a8;
+            if (a8 + 8 <= p.A) {
+                st_chunk(drow, ld_chunk(srow));
+            } else {
+                for (int e = 0; a8 + e < p.A; ++e) drow[e] = srow[e];
+            }
         }
     }
 }
 
 template <typename T>
 int launch_decode_t(const DecodeArgs& a, hipStream_t s) {
-    const long long n = (long long)a.B * a.A;
-    hipLaunchKernelGGL((head_decode<T>), dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, a);
+    const dim3 g((unsigned)((a.A + 255) / 256), (unsigned)a.B);
+    const int lds = (4 + a.nc) * 256 * (int)sizeof(T);
+    if (a.A % 8 == 0 && lds <= 64 * 1024) {
+        hipLaunchKernelGGL((head_decode<T, true>), g, dim3(256), lds, s, a);
+    } else {
+        hipLaunchKernelGGL((head_decode<T, false>), g, dim3(256), 0, s, a);
+    }
     return (int)hipGetLastError();
 }
 
