@@ -169,11 +169,12 @@ int yh_set_graph(yh_handle* h, int enable);
 /* Kernel that runs op `index` at (batch, height, width): for dense convs the
  * implementation the per-shape tuner picked on the first yh_forward at that
  * shape ("gemm", "gemm64", "gemm128", "stream", "direct", "stream4",
- * "stream8"; all bit-identical), for the other ops the op's single kernel name.
+ * "stream8", "tiny"; all bit-identical; a layer may instead run "ksplit4",
+ * chosen by a fixed shape rule), for the other ops the op's single kernel name.
  * YH_ESTATE before that forward. */
 int yh_op_kernel(const yh_handle* h, int index, int batch, int height, int width, const char** name);
 
-/* Force dense-conv kernel `kernel` (0..6, the order of the names above) on every
+/* Force dense-conv kernel `kernel` (0..7, the order of the names above) on every
  * conv that supports it (the others run "gemm"), or -1 to return to per-shape
  * autotuning. Drops the tuned choices and captured graphs. Testing hook: every
  * kernel must produce bit-identical outputs. */

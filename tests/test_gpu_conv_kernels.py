@@ -1,8 +1,8 @@
 """Every dense-conv kernel implementation gives bit-identical forwards. Marked gpu.
 
 The per-shape autotuner (csrc/engine.cpp ensure_tuned) may pick any of
-conv_gemm2 (3 tile shapes), conv_stream (2-, 4- and 8-slot rings) and
-conv_direct per layer. That is only valid because they all accumulate K in the
+conv_gemm2 (3 tile shapes), conv_stream (2-, 4- and 8-slot rings),
+conv_direct and conv_tiny per layer. That is only valid because they all accumulate K in the
 same order (32-deep MFMA steps, increasing k): this test forces each one on
 every layer that supports it and requires the exact same head output as the
 reference kernel (conv_gemm2), which the forward parity tests pin to the oracle.
@@ -14,7 +14,7 @@ from yolo_hip import synth
 
 pytestmark = pytest.mark.gpu
 
-KERNELS = ["gemm", "gemm64", "gemm128", "stream", "direct", "stream4", "stream8"]
+KERNELS = ["gemm", "gemm64", "gemm128", "stream", "direct", "stream4", "stream8", "tiny"]
 
 
 @pytest.mark.parametrize("dtype,batch", [(torch.bfloat16, 32), (torch.float16, 4)])

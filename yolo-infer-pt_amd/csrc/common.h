@@ -151,7 +151,8 @@ enum ConvKernel {
     CONV_DIRECT = 4,   // conv_direct, LDS-resident weights, register-streamed pixels
     CONV_STREAM4 = 5,  // conv_stream, 4-slot ring (3 K stages in flight)
     CONV_STREAM8 = 6,  // conv_stream, 8-slot ring (7 K stages in flight)
-    CONV_NKERNELS = 7
+    CONV_TINY = 7,     // conv_tiny, 3x3 stride 1 with Cin <= 32: input rows staged in LDS
+    CONV_NKERNELS = 8
 };
 
 // launchers (return hipError_t as int)

@@ -982,6 +982,220 @@ int launch_direct(const ConvArgs& a, hipStream_t s) {
 }
 
 // ---------------------------------------------------------------------------
+// conv_tiny: 3x3 stride-1 convs with few input channels (Cin = 8 / 16 / 32, e.g.
+// the 160x160 and 80x80 C3k2 bottlenecks 16->8->16 and 32->16->32). A
+// workgroup owns TH full output rows of one image and one cout slice: the weight
+// slice and the input rows (+1 halo row / column, zero border) are staged in LDS
+// once with all loads in flight. The k-table is the same for every pixel, so each
+// lane turns its k-steps into LDS offsets once (padding steps point at a zero
+// chunk); a job's fragment reads are then independent ds_read_b128s from one base.
+// K order and epilogue are conv_direct's -> bit-identical outputs.
+struct TinyPlan {
+    int TH, PC, pst, nrb, ntl, slices, B, lds, zoff;
+};
+constexpr int TINY_NT = 256;
+constexpr int TINY_BUDGET = 64 * 1024;   // two or more workgroups per CU
+constexpr int TINY_KS = 10;              // k-steps: Kp <= 320 (Cin <= 32)
+
+template <typename T, int NTL>
+__global__ __launch_bounds__(TINY_NT) void conv_tiny(const ConvArgs p, const TinyPlan g) {
+    static_assert(sizeof(T) == 2, "16-bit path");
+    constexpr int BN = NTL * 16, RUN = 4 * NTL, MT = 2;
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const int ldw = p.Kp * 2 + 16;
+    const int kc8 = p.Kp / 8;
+    char* wl = smem;                     // BN rows x ldw
+    char* pl = smem + BN * ldw;          // patch, then a 16-B zero chunk at g.zoff
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int p16 = lane & 15, q = lane >> 4;
+    const int bid = blockIdx.x;
+    const int slice = bid % g.slices, rem = bid / g.slices;
+    const int n = rem / g.nrb, rb = rem - n * g.nrb;
+    const int ho0 = rb * g.TH, th = min(g.TH, p.Ho - ho0);
+    const int n0 = slice * BN;
+    const int cpp = p.c0 / 8;   // 16-B chunks per input pixel
+    {   // weights (rows permuted as conv_direct) and input rows: loads first, then stores
+        const T* wg = reinterpret_cast<const T*>(p.w);
+        constexpr int FB = 8;
+        const int wtot = BN * kc8;
+        for (int c0 = tid; c0 < wtot; c0 += TINY_NT * FB) {
+            uint4 v[FB];
+            int dst[FB];
+#pragma unroll
+            for (int u = 0; u < FB; ++u) {
+                const int c = min(c0 + u * TINY_NT, wtot - 1);
+                const int R = c / kc8, kc = c - R * kc8;
+                const int i = R >> 4, qq = (R >> 2) & 3, r = R & 3;
+                const int co = n0 + qq * RUN + 4 * i + r;
+                v[u] = *reinterpret_cast<const uint4*>(wg + (long long)co * p.Kp + kc * 8);
+                dst[u] = R * ldw + kc * 16;
+            }
+#pragma unroll
+            for (int u = 0; u < FB; ++u) *reinterpret_cast<uint4*>(wl + dst[u]) = v[u];
+        }
+        const T* in0 = reinterpret_cast<const T*>(p.in0) + (long long)n * p.h0 * p.w0 * p.ldc0;
+        const int hi0 = ho0 - 1;
+        const int ptot = (th + 2) * g.PC * cpp;
+        for (int c0 = tid; c0 < ptot; c0 += TINY_NT * FB) {
+            uint4 v[FB];
+            int dst[FB];
+            bool ok[FB];
+#pragma unroll
+            for (int u = 0; u < FB; ++u) {
+                const int cc = min(c0 + u * TINY_NT, ptot - 1);
+                const int px = cc / cpp, ch = cc - px * cpp;
+                const int pr = px / g.PC, pc = px - pr * g.PC;
+                const int hi = hi0 + pr, wi = pc - 1;
+                ok[u] = (unsigned)hi < (unsigned)p.Hi && (unsigned)wi < (unsigned)p.Wi;
+                const int hc = min(max(hi, 0), p.Hi - 1), wc = min(max(wi, 0), p.Wi - 1);
+                v[u] = *reinterpret_cast<const uint4*>(in0 + ((long long)hc * p.w0 + wc) * p.ldc0 + ch * 8);
+                dst[u] = px * g.pst + ch * 16;
+            }
+#pragma unroll
+            for (int u = 0; u < FB; ++u)
+                *reinterpret_cast<uint4*>(pl + dst[u]) = ok[u] ? v[u] : make_uint4(0, 0, 0, 0);
+        }
+        if (tid == 0) *reinterpret_cast<uint4*>(pl + g.zoff) = make_uint4(0, 0, 0, 0);
+    }
+    // this lane's k-steps as patch offsets relative to the pixel's (r, c) tap-(0,0) base;
+    // padding steps read the zero chunk (an absolute offset: base is subtracted back)
+    const int nks = (p.K + 31) / 32;
+    int toff[TINY_KS];
+    bool tpad[TINY_KS];
+#pragma unroll
+    for (int k = 0; k < TINY_KS; ++k) {
+        const int e = k < nks ? p.ktab[k * 4 + q] : 0xffff;
+        const int kh = e >> 24, kw = (e >> 16) & 0xff, ci = e & 0xffff;
+        tpad[k] = ci == 0xffff;
+        toff[k] = tpad[k] ? 0 : (kh * g.PC + kw) * g.pst + ci * 2;
+    }
+    __syncthreads();
+    const int npx = th * p.Wo;
+    const int njob = (npx + 16 * MT - 1) / (16 * MT);
+    const int co = n0 + q * RUN;
+    const char* wrow = wl + p16 * ldw + q * 16;
+    float bv[RUN];
+#pragma unroll
+    for (int e = 0; e < RUN; ++e) bv[e] = co + e < p.Cout ? p.bias[co + e] : 0.f;
+    const T* res = reinterpret_cast<const T*>(p.res);
+    T* out = reinterpret_cast<T*>(p.out);
+    for (int job = wave; job < njob; job += TINY_NT / 64) {
+        int mg[MT];
+        const char* base[MT];
+#pragma unroll
+        for (int j = 0; j < MT; ++j) {
+            const int idx = (job * MT + j) * 16 + p16;
+            const bool v = idx < npx;
+            const int r = v ? idx / p.Wo : 0, c = v ? idx - r * p.Wo : 0;
+            base[j] = pl + (r * g.PC + c) * g.pst;
+            mg[j] = v ? (n * p.Ho + ho0 + r) * p.Wo + c : -1;
+        }
+        f32x4 acc[NTL][MT];
+#pragma unroll
+        for (int i = 0; i < NTL; ++i)
+#pragma unroll
+            for (int j = 0; j < MT; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+        uint4 xa[TINY_KS][MT];
+#pragma unroll
+        for (int k = 0; k < TINY_KS; ++k)
+#pragma unroll
+            for (int j = 0; j < MT; ++j)
+                xa[k][j] = *reinterpret_cast<const uint4*>(tpad[k] ? pl + g.zoff : base[j] + toff[k]);
+        // all TINY_KS steps, branch-free: steps past K read the zero chunk against a
+        // clamped (finite) weight step and add exactly 0
+        const int kmax = p.Kp / 32 - 1;
+#pragma unroll
+        for (int k = 0; k < TINY_KS; ++k) {
+            uint4 wf[NTL];
+#pragma unroll
+            for (int i = 0; i < NTL; ++i)
+                wf[i] = *reinterpret_cast<const uint4*>(wrow + i * 16 * ldw + min(k, kmax) * 64);
+#pragma unroll
+            for (int j = 0; j < MT; ++j)
+#pragma unroll
+                for (int i = 0; i < NTL; ++i) Mma<T>::step(acc[i][j], &wf[i], &xa[k][j]);
+        }
+        if (co >= p.Cout) continue;
+#pragma unroll
+        for (int j = 0; j < MT; ++j) {
+            const int m = mg[j];
+            if (m < 0) continue;
+            float vv[RUN];
+#pragma unroll
+            for (int e = 0; e < RUN; ++e) {
+                float x = acc[e >> 2][j][e & 3] + bv[e];
+                if (p.act == ACT_SILU) x = silu<T>(x);
+                vv[e] = x;
+            }
+            if constexpr (RUN >= 8) {
+#pragma unroll
+                for (int c8 = 0; c8 < RUN / 8; ++c8) {
+                    if (co + c8 * 8 >= p.Cout) break;
+                    float f[8];
+#pragma unroll
+                    for (int e = 0; e < 8; ++e) f[e] = fromf_round<T>(vv[c8 * 8 + e]);
+                    if (res) {
+                        float gg[8];
+                        chunk_to_f(ld_chunk(res + (long long)m * p.ldr + co + c8 * 8), gg);
+#pragma unroll
+                        for (int e = 0; e < 8; ++e) f[e] += gg[e];
+                    }
+                    st_chunk(out + (long long)m * p.ldo + co + c8 * 8, f_to_chunk<T>(f));
+                }
+            } else {
+                T o[4];
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    float x = fromf_round<T>(vv[e]);
+                    if (res) x += tof(res[(long long)m * p.ldr + co + e]);
+                    o[e] = fromf<T>(x);
+                }
+                *reinterpret_cast<uint2*>(out + (long long)m * p.ldo + co) = *reinterpret_cast<const uint2*>(o);
+            }
+        }
+    }
+}
+
+bool tiny_plan(const ConvArgs& a, TinyPlan* out) {
+    if (!(a.KH == 3 && a.KW == 3 && a.pad == 1 && a.stride == 1)) return false;
+    if (a.c1 != 0 || a.up0 != 0 || a.c0 % 8 != 0 || a.c0 > 32 || a.Cin != a.c0) return false;
+    if (a.Hi != a.h0 || a.Wi != a.w0 || a.Hi != a.Ho || a.Wi != a.Wo) return false;
+    if ((a.K + 31) / 32 > TINY_KS) return false;
+    TinyPlan g{};
+    g.ntl = a.Cout <= 16 ? 1 : a.Cout <= 32 ? 2 : 4;
+    g.PC = a.Wi + 2;
+    g.pst = a.c0 * 2 + 16;
+    const int wbytes = 16 * g.ntl * (a.Kp * 2 + 16);
+    int th = 0;
+    for (int t = 1; t <= a.Ho; ++t) {
+        if (wbytes + (t + 2) * g.PC * g.pst + 16 > TINY_BUDGET) break;
+        th = t;
+    }
+    if (th == 0) return false;
+    g.nrb = (a.Ho + th - 1) / th;
+    g.TH = (a.Ho + g.nrb - 1) / g.nrb;
+    g.slices = (a.Cout + 16 * g.ntl - 1) / (16 * g.ntl);
+    g.B = a.M / (a.Ho * a.Wo);
+    g.zoff = (g.TH + 2) * g.PC * g.pst;
+    g.lds = wbytes + g.zoff + 16;
+    if (out) *out = g;
+    return true;
+}
+
+template <typename T>
+int launch_tiny(const ConvArgs& a, hipStream_t s) {
+    TinyPlan g{};
+    if (!tiny_plan(a, &g)) return (int)hipErrorInvalidValue;
+    const dim3 grid((unsigned)(g.B * g.nrb * g.slices));
+    switch (g.ntl) {
+        case 1: hipLaunchKernelGGL((conv_tiny<T, 1>), grid, dim3(TINY_NT), g.lds, s, a, g); break;
+        case 2: hipLaunchKernelGGL((conv_tiny<T, 2>), grid, dim3(TINY_NT), g.lds, s, a, g); break;
+        default: hipLaunchKernelGGL((conv_tiny<T, 4>), grid, dim3(TINY_NT), g.lds, s, a, g); break;
+    }
+    return (int)hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
 // conv_gemm2k: conv_gemm2 (BM 64) with the K walk split over the workgroup's
 // waves, for layers whose few tiles leave CUs idle and whose long K loop is a
 // chain of LDS-DMA round trips (e.g. head.box.2.0: 200 tiles, 36 stages).
@@ -1599,6 +1813,7 @@ bool conv_kernel_ok(int dtype, int kern, const ConvArgs& a) {
     if (a.Kp % BK2 != 0) return false;
     if (dtype == F32) return kern == CONV_GEMM;
     if (kern == CONV_DIRECT) return direct_plan(a, nullptr, nullptr);
+    if (kern == CONV_TINY) return tiny_plan(a, nullptr);
     if (kern == CONV_STREAM4 || kern == CONV_STREAM8) {
         // deep rings only pay off while the tiles leave CUs idle; LDS must fit
         const int BN = a.Cout <= 16 ? 16 : a.Cout <= 32 ? 32 : a.Cout <= 64 ? 64 : 128;
@@ -1639,6 +1854,8 @@ int launch_conv(int dtype, int kern, int BM, int BN, const ConvArgs& a, hipStrea
         }
         case CONV_DIRECT:
             return h ? launch_direct<_Float16>(a, s) : launch_direct<__bf16>(a, s);
+        case CONV_TINY:
+            return h ? launch_tiny<_Float16>(a, s) : launch_tiny<__bf16>(a, s);
     }
     return (int)hipErrorInvalidValue;
 }

@@ -1831,7 +1831,7 @@ int yh_op_kernel(const yh_handle* h, int index, int batch, int height, int width
     return guarded([&] {
         yh::require(h && index >= 0 && index < (int)h->net.ops.size(), "op index out of range");
         const yh::Net& n = h->net;
-        static const char* conv_names[] = {"gemm", "gemm64", "gemm128", "stream", "direct", "stream4", "stream8"};
+        static const char* conv_names[] = {"gemm", "gemm64", "gemm128", "stream", "direct", "stream4", "stream8", "tiny"};
         static const char* op_names[] = {"stem", "conv", "dwconv", "sppf", "attention", "decode"};
         const yh::Op& op = n.ops[index];
         if (op.kind != yh::OP_CONV) {

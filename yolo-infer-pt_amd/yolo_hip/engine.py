@@ -151,7 +151,7 @@ class Engine:
         check(lib().yh_set_graph(self._h, int(bool(enable))))
 
     def force_conv_kernel(self, kernel):
-        """Run dense convs on one kernel implementation (0..6), or -1 for per-shape autotuning."""
+        """Run dense convs on one kernel implementation (0..7), or -1 for per-shape autotuning."""
         check(lib().yh_force_conv_kernel(self._h, int(kernel)), "force_conv_kernel")
 
     def set_level_fusion(self, enable):
