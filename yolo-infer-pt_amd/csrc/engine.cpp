@@ -1267,32 +1267,40 @@ struct Net {
     // against the channel-range dependencies of every unit. YH_HEADSPLIT=0 turns it off.
     bool head_split = [] { const char* e = getenv("YH_HEADSPLIT"); return !e || atoi(e) != 0; }();
     hipStream_t hs_stream = nullptr;
-    hipEvent_t hs_ev[2] = {nullptr, nullptr};
+    hipEvent_t hs_ev[3] = {nullptr, nullptr, nullptr};
     // segment of each unit (0 A, 1 B, 2 C, 3 D) if the plan splits cleanly, else empty
+    // happens-before between segments under forward_head_split's launch order
+    //   s0: A(0) -eA-> C1(2) -eC-> C3(4) -(wait eB)-> D(5);  s1: (wait eA) B0(1) (wait eC) B1(3) -eB->
+    static bool seg_before(int a, int b) {
+        static const bool hb[6][6] = {
+            {0, 1, 1, 1, 1, 1}, {0, 0, 0, 1, 0, 1}, {0, 0, 0, 1, 1, 1},
+            {0, 0, 0, 0, 0, 1}, {0, 0, 0, 0, 0, 1}, {0, 0, 0, 0, 0, 0}};
+        return hb[a][b];
+    }
     std::vector<int> head_segments() const {
         const auto& us = cur_plan->units;
         const int n = (int)us.size();
-        std::vector<int> seg(n, 0);
-        int last_a = -1;
+        std::vector<int> seg(n, -1);
+        int last_h2 = -1, last_h4 = -1;
         for (int j = 0; j < n; ++j) {
             const Unit& u = us[j];
             const std::string& lb = ops[u.first].label;
-            const bool h0 = lb.rfind("head.box.0.", 0) == 0 || lb.rfind("head.cls.0.", 0) == 0;
+            auto pre = [&](const char* x) { return lb.rfind(x, 0) == 0; };
+            const bool h0 = pre("head.box.0.") || pre("head.cls.0."), h1 = pre("head.box.1.") || pre("head.cls.1.");
             const bool dec = ops[u.first].kind == OP_DECODE;
-            if (u.level && (h0 || dec)) return {};   // a fused level unit spans segments
-            for (int k = u.first; k < u.last; ++k)
-                if (ops[k].label.rfind("fpn.h2", 0) == 0) last_a = j;
-            seg[j] = h0 ? 1 : dec ? 3 : 0;
+            if (u.level && (h0 || h1 || dec)) return {};   // a fused level unit spans segments
+            for (int k = u.first; k < u.last; ++k) {
+                if (ops[k].label.rfind("fpn.h2", 0) == 0) last_h2 = j;
+                if (ops[k].label.rfind("fpn.h4", 0) == 0) last_h4 = j;
+            }
+            seg[j] = h0 ? 1 : h1 ? 3 : dec ? 5 : -1;
         }
-        if (last_a < 0 || seg[n - 1] != 3) return {};
-        for (int j = last_a + 1; j < n; ++j)
-            if (seg[j] == 0) seg[j] = 2;
-        for (int j = 0; j <= last_a; ++j)
-            if (seg[j] != 0) return {};               // head work before the split point
+        if (last_h2 < 0 || last_h4 < last_h2 || seg[n - 1] != 5) return {};
+        for (int j = 0; j < n; ++j)
+            if (seg[j] < 0) seg[j] = j <= last_h2 ? 0 : j <= last_h4 ? 2 : 4;
         for (int j = 0; j < n - 1; ++j)
-            if (seg[j] == 3) return {};
-        // every dependency must run forward along the segment order A -> {B, C} -> D,
-        // and nothing may link B and C
+            if (seg[j] == 5) return {};
+        // every dependency must follow the segments' happens-before order
         std::vector<std::vector<Rg>> rd(n), wr(n);
         for (int j = 0; j < n; ++j) unit_regions(us[j], rd[j], wr[j]);
         auto ov = [](const std::vector<Rg>& a, const std::vector<Rg>& b) {
@@ -1304,9 +1312,7 @@ struct Net {
         for (int j = 0; j < n; ++j)
             for (int i = 0; i < j; ++i) {
                 if (!(ov(wr[i], rd[j]) || ov(rd[i], wr[j]) || ov(wr[i], wr[j]))) continue;
-                const int si = seg[i], sj = seg[j];
-                const bool ok = si == sj || si == 0 || sj == 3;
-                if (!ok) return {};
+                if (seg[i] != seg[j] && !seg_before(seg[i], seg[j])) return {};
             }
         return seg;
     }
@@ -1336,7 +1342,7 @@ struct Net {
             const std::vector<int> seg = head_segments();
             if (seg.empty()) return false;
             run_ops(B, H, W, s);   // eager pass: first launches outside any capture
-            for (int w = 0; w < 4; ++w)
+            for (int w = 0; w < 6; ++w)
                 graphs.emplace(GraphKey{B, H, W, in_u8 | ((w + 1) << 1)}, capture_segment(seg, w, B, H, W));
             if (!hs_stream) HIPCHECK(hipStreamCreateWithFlags(&hs_stream, hipStreamNonBlocking));
             for (auto& e : hs_ev)
@@ -1346,11 +1352,15 @@ struct Net {
         HIPCHECK(hipGraphLaunch(g(0), s));              // A: backbone + FPN top-down
         HIPCHECK(hipEventRecord(hs_ev[0], s));
         HIPCHECK(hipStreamWaitEvent(hs_stream, hs_ev[0], 0));
-        HIPCHECK(hipGraphLaunch(g(1), hs_stream));      // B: 80x80 head, beside C
-        HIPCHECK(hipEventRecord(hs_ev[1], hs_stream));
-        HIPCHECK(hipGraphLaunch(g(2), s));              // C: FPN bottom-up + small heads
-        HIPCHECK(hipStreamWaitEvent(s, hs_ev[1], 0));
-        HIPCHECK(hipGraphLaunch(g(3), s));              // D: decode
+        HIPCHECK(hipGraphLaunch(g(1), hs_stream));      // B0: 80x80 head
+        HIPCHECK(hipGraphLaunch(g(2), s));              // C1: fpn.h3, fpn.h4
+        HIPCHECK(hipEventRecord(hs_ev[1], s));
+        HIPCHECK(hipStreamWaitEvent(hs_stream, hs_ev[1], 0));
+        HIPCHECK(hipGraphLaunch(g(3), hs_stream));      // B1: 40x40 head
+        HIPCHECK(hipEventRecord(hs_ev[2], hs_stream));
+        HIPCHECK(hipGraphLaunch(g(4), s));              // C3: fpn.h5, fpn.h6, 20x20 head
+        HIPCHECK(hipStreamWaitEvent(s, hs_ev[2], 0));
+        HIPCHECK(hipGraphLaunch(g(5), s));              // D: decode
         return true;
     }
 
