@@ -1661,10 +1661,146 @@ __global__ __launch_bounds__(STEM_TW) void conv_first_mfma(const FirstConvArgs p
     }
 }
 
+// 16-bit stem, 2-D tiles: a workgroup = STEM2_TR output rows x STEM2_TW pixels.
+// The 2*TR+1 input rows of each channel are staged once as T (the values the
+// MFMA consumes), so neighbouring output rows share their overlap row in LDS
+// (input read ~(2TR+1)/(2TR) times instead of 1.5x) and every thread keeps
+// STEM2_NCH 16-B loads in flight. Same k order (ci, kh, kw) and epilogue as
+// conv_first_mfma -> identical outputs.
+constexpr int STEM2_TW = 160, STEM2_NT = 256;
+constexpr int STEM2_SEG = 2 * STEM2_TW + 16;         // staged columns per row segment
+constexpr int STEM2_CPS = STEM2_SEG / 8;             // 8-element chunks per segment
+template <typename T, typename U, int NT, int STEM2_TR>
+__global__ __launch_bounds__(STEM2_NT) void conv_first_tile(const FirstConvArgs p) {
+    constexpr int STEM2_ROWS = 3 * (2 * STEM2_TR + 1);   // (channel, input row) segments
+    constexpr int STEM2_NCH = (STEM2_ROWS * STEM2_CPS + STEM2_NT - 1) / STEM2_NT;
+    static_assert(sizeof(T) == 2, "16-bit path");
+    __shared__ __attribute__((aligned(16))) T patch[STEM2_ROWS][STEM2_SEG];
+    const int wo0 = blockIdx.x * STEM2_TW, ho0 = blockIdx.y * STEM2_TR, n = blockIdx.z;
+    const U* x = reinterpret_cast<const U*>(p.io[0]);
+    const int col0 = 2 * wo0 - 8;
+    const long long plane = (long long)p.H * p.W;
+    {   // stage: all loads first (clamped address + select), then the LDS stores
+        using Raw = typename std::conditional<sizeof(U) == 1, uint2, uint4>::type;   // 8 elements
+        Raw raw[STEM2_NCH];
+        bool ok[STEM2_NCH];
+        int dst[STEM2_NCH];
+#pragma unroll
+        for (int u = 0; u < STEM2_NCH; ++u) {
+            const int c = min((int)threadIdx.x + u * STEM2_NT, STEM2_ROWS * STEM2_CPS - 1);
+            const int seg = c / STEM2_CPS, ch = c - seg * STEM2_CPS;
+            const int ci = seg / (2 * STEM2_TR + 1), rr = seg - ci * (2 * STEM2_TR + 1);
+            const int hi = 2 * ho0 - 1 + rr;
+            const int col = col0 + ch * 8;
+            ok[u] = hi >= 0 && hi < p.H && col >= 0 && col + 8 <= p.W;
+            const int hc = min(max(hi, 0), p.H - 1), cc = min(max(col, 0), p.W - 8);
+            raw[u] = *reinterpret_cast<const Raw*>(x + ((long long)n * 3 + ci) * plane + (long long)hc * p.W + cc);
+            dst[u] = c;
+        }
+#pragma unroll
+        for (int u = 0; u < STEM2_NCH; ++u) {
+            const int seg = dst[u] / STEM2_CPS, ch = dst[u] - seg * STEM2_CPS;
+            uint4 v;
+            if constexpr (sizeof(U) == 1) {
+                float f[8];
+#pragma unroll
+                for (int e = 0; e < 8; ++e)
+                    f[e] = stem_in<uint8_t, T>((uint8_t)(((e < 4 ? raw[u].x : raw[u].y) >> (8 * (e & 3))) & 255u));
+                v = f_to_chunk<T>(f).v[0];
+            } else {
+                v = raw[u];
+            }
+            *reinterpret_cast<uint4*>(&patch[seg][ch * 8]) = ok[u] ? v : make_uint4(0, 0, 0, 0);
+        }
+    }
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int fr = lane & 15, g = lane >> 4;
+    uint4 wf[NT];
+#pragma unroll
+    for (int i = 0; i < NT; ++i) {
+        float f[8];
+        const int co = 16 * i + fr;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const int k = 8 * g + j;
+            f[j] = (k < 27 && co < p.Cout) ? p.w[k * p.Cout + co] : 0.f;
+        }
+        wf[i] = f_to_chunk<T>(f).v[0];
+    }
+    float bv[NT][4];
+#pragma unroll
+    for (int i = 0; i < NT; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int co = 16 * i + 4 * g + r;
+            bv[i][r] = co < p.Cout ? p.bias[co] : 0.f;
+        }
+    // this lane's 8 k values as (segment row offset, column offset) in the patch
+    int koff[8];
+    bool kok[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        const int k = 8 * g + j;
+        const int ci = k / 9, kh = (k - ci * 9) / 3, kw = k - ci * 9 - kh * 3;
+        kok[j] = k < 27;
+        koff[j] = kok[j] ? (ci * (2 * STEM2_TR + 1) + kh) * STEM2_SEG + kw : 0;
+    }
+    __syncthreads();
+    const T* pbase = &patch[0][0];
+    constexpr int GPR = STEM2_TW / 16;                 // 16-pixel groups per output row
+    constexpr int NG = STEM2_TR * GPR / (STEM2_NT / 64);
+#pragma unroll 2
+    for (int it = 0; it < NG; ++it) {
+        const int gi = wave + it * (STEM2_NT / 64);
+        const int tr = gi / GPR, px = (gi - tr * GPR) * 16 + fr;
+        const int ho = ho0 + tr, wo = wo0 + px;
+        const int b0 = 2 * tr * STEM2_SEG + 2 * px - 1 + 8;
+        T xv[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) xv[j] = kok[j] ? pbase[b0 + koff[j]] : fromf<T>(0.f);
+        const uint4 xf = *reinterpret_cast<const uint4*>(xv);
+        const long long m = ((long long)n * p.Ho + ho) * p.Wo + wo;
+        T* out = reinterpret_cast<T*>(p.out) + m * p.ldo;
+        const bool live = wo < p.Wo && ho < p.Ho;
+#pragma unroll
+        for (int i = 0; i < NT; ++i) {
+            f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+            Mma<T>::step(acc, &wf[i], &xf);
+            const int co = 16 * i + 4 * g;
+            if (live && co < p.Cout) {
+                unsigned u[4];
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    float v = acc[r] + bv[i][r];
+                    if (p.act == ACT_SILU) v = silu<T>(v);
+                    u[r] = (unsigned short)__builtin_bit_cast(short, fromf<T>(v));
+                }
+                *reinterpret_cast<uint2*>(out + co) = make_uint2(u[0] | (u[1] << 16), u[2] | (u[3] << 16));
+            }
+        }
+    }
+}
+
 template <typename T, typename U>
 int launch_first_tu(const FirstConvArgs& a, int B, hipStream_t s) {
     const dim3 grid((a.Wo + STEM_TW - 1) / STEM_TW, a.Ho, B);
     if constexpr (sizeof(T) == 2) {
+        static const bool tile = [] { const char* e = getenv("YH_STEM"); return !e || atoi(e) != 1; }();
+        if (tile) {
+            static const int tr = [] { const char* e = getenv("YH_STEM_TR"); return e ? atoi(e) : 4; }();
+            const dim3 g2((a.Wo + STEM2_TW - 1) / STEM2_TW, (a.Ho + tr - 1) / tr, B);
+#define YH_ST(R)                                                                                              \
+            switch ((a.Cout + 15) / 16) {                                                                     \
+                case 1: hipLaunchKernelGGL((conv_first_tile<T, U, 1, R>), g2, dim3(STEM2_NT), 0, s, a); break; \
+                case 2: hipLaunchKernelGGL((conv_first_tile<T, U, 2, R>), g2, dim3(STEM2_NT), 0, s, a); break; \
+                case 4: hipLaunchKernelGGL((conv_first_tile<T, U, 4, R>), g2, dim3(STEM2_NT), 0, s, a); break; \
+                case 6: hipLaunchKernelGGL((conv_first_tile<T, U, 6, R>), g2, dim3(STEM2_NT), 0, s, a); break; \
+                default: return (int)hipErrorInvalidValue;                                                    \
+            }
+            if (tr == 2) { YH_ST(2) } else if (tr == 8) { YH_ST(8) } else { YH_ST(4) }
+#undef YH_ST
+            return (int)hipGetLastError();
+        }
         switch ((a.Cout + 15) / 16) {
             case 1: hipLaunchKernelGGL((conv_first_mfma<T, U, 1>), grid, dim3(STEM_TW), 0, s, a); break;
             case 2: hipLaunchKernelGGL((conv_first_mfma<T, U, 2>), grid, dim3(STEM_TW), 0, s, a); break;
