@@ -4,10 +4,14 @@ BASELINE.json metric: images/sec at 640x640 batch 32, v11_n, 1/2/4/8 MI355X.
 A step = one pass of the hot path over one batch resident in HBM: the HIP
 forward (yh_forward, replayed as a HIP graph), the on-device NMS (yh_nms) and,
 for N > 1, the RCCL gather of the fixed-size detection buffers to rank 0.
-By default steps are pipelined over two streams (yolo_hip.pipeline): the NMS
-(+ gather) of batch k runs beside the forward of batch k+1; every batch still
-gets its full forward and NMS inside the timed region. --serial runs them back
-to back on one stream.
+By default steps are pipelined (yolo_hip.pipeline) over 3 forward lanes - three
+engines (own workspace and HIP graphs, same weights), batch k on lane k % 3 -
+plus one NMS stream: the forwards of consecutive batches overlap, so one
+batch's latency-bound 40x40 / 20x20 layers share the chip with another's
+large layers, and the NMS (+ gather) of batch k runs beside them. Every batch
+still gets its full forward and NMS inside the timed region. --lanes 1 is the
+two-stream pipeline (forward k+1 beside NMS k); --serial runs forward and NMS
+back to back on one stream.
 Data-parallel: every rank processes its own batch of 32 (weak scaling).
 
   python bench.py [--gpus N] [--steps K] [--warmup W]
@@ -153,6 +157,11 @@ def main():
     ap.add_argument("--profile-steps", type=int, default=None)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-roofline", action="store_true")
+    ap.add_argument("--lanes", type=int, default=3,
+                    help="forward lanes: engines whose forwards of consecutive batches overlap "
+                         "(measured r01, v11_n b32: 1 -> 20.3k, 2 -> 23.2k, 3 -> 27.2k, 4 -> 25.2k img/s)")
+    ap.add_argument("--nms-on-lane", action="store_true",
+                    help="run each batch's NMS on its forward lane's stream (no separate NMS stream)")
     ap.add_argument("--serial", action="store_true",
                     help="run forward and NMS back to back on one stream (no batch-to-batch overlap)")
     args = ap.parse_args()
@@ -172,6 +181,12 @@ def main():
     from yolo_hip.engine import Engine, nms
     from yolo_hip.pipeline import DetectPipeline
 
+    if args.lanes > 1 and not args.serial:
+        # The lanes supply the concurrency the segment split (YH_HEADSPLIT, a second stream
+        # per engine) would: keep lanes + the NMS stream within the 4 HIP hardware queues.
+        os.environ.setdefault("YH_HEADSPLIT", "0")
+    else:
+        args.lanes = 1
     model = build_model(args.variant)
     eng = Engine(*model._yh_arch, dev, dtype)
     eng.load_module(model)
@@ -184,7 +199,16 @@ def main():
     gather = Gather(B, 300, dev, rank, world)
 
     post = (lambda d, c: gather(d, c)) if dist else None  # RCCL gather of the fixed-size results to rank 0
-    pipe = DetectPipeline(eng, B, S, S, post=post)
+    engs = [eng]
+    for _ in range(args.lanes - 1):
+        e = Engine(*model._yh_arch, dev, dtype)
+        e.load_module(model)
+        e.reserve(B, S, S)
+        engs.append(e)
+    for e in engs:   # tune + capture each lane's graphs one at a time, before any overlap
+        e.forward(x, out=y)
+        torch.cuda.synchronize()
+    pipe = DetectPipeline(engs, B, S, S, post=post, nms_on_lane=args.nms_on_lane)
 
     def step():
         if args.serial:
@@ -247,7 +271,9 @@ def main():
                        "parallelism": f"dp{world}", "nms": "on-device, conf 0.001, iou 0.65, max_det 300"},
             "roofline": roof,
             "cpu_baseline": cpu,
-            "schedule": "serial" if args.serial else "2-stream pipeline (forward k+1 overlaps NMS k)",
+            "schedule": "serial" if args.serial else (
+                "2-stream pipeline (forward k+1 overlaps NMS k)" if args.lanes == 1 else
+                f"{args.lanes} forward lanes (forwards of consecutive batches overlap) + NMS stream"),
             "kept_last_step": kept[:4],
         }
         print(json.dumps(rec), flush=True)

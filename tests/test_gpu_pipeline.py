@@ -1,4 +1,5 @@
-"""Two-stream DetectPipeline (forward k+1 beside NMS k) vs the sequential schedule,
+"""Two-stream DetectPipeline (forward k+1 beside NMS k), and with two forward lanes
+(forwards of consecutive batches overlap on two engines), vs the sequential schedule,
 at the bench's full size (v11_n, 640x640, batch 32, bf16). Marked gpu.
 
 Bar: bit-identical detections and counts for every batch - the pipeline only
@@ -40,6 +41,33 @@ def test_pipeline_equals_sequential(gpu, engine):
         want.append((d.cpu(), c.cpu()))
     pipe = DetectPipeline(engine, B, S, S)
     got = [pipe.submit(x) for x in xs + xs[:1]]   # 4 batches: buffer reuse is exercised
+    torch.cuda.synchronize()
+    for i, (d, c, _, _) in enumerate(got):
+        wd, wc = want[i % 3]
+        assert torch.equal(c.cpu(), wc), f"batch {i}: counts differ"
+        for j, k in enumerate(wc.tolist()):
+            assert torch.equal(d[j, :k].cpu(), wd[j, :k]), f"batch {i} image {j}"
+
+
+def test_two_lane_pipeline_equals_sequential(gpu, engine):
+    from nets import nn
+    from yolo_hip.engine import Engine, nms
+    from yolo_hip.pipeline import DetectPipeline
+    B, S = 32, 640
+    torch.manual_seed(0)
+    model = nn.yolo_v11_n(80)
+    model.load_state_dict(synth.synth_state_dict(model.state_dict(), seed=0))
+    model.eval()
+    lane1 = Engine(*model._yh_arch, gpu, torch.bfloat16)
+    lane1.load_module(model)
+    xs = [synth.synth_scenes(B, S, S, seed=210 + i).to(gpu, torch.bfloat16) for i in range(3)]
+    want = []
+    for x in xs:
+        d, c = nms(engine.forward(x))
+        want.append((d.cpu(), c.cpu()))
+    pipe = DetectPipeline([engine, lane1], B, S, S)
+    got = [pipe.submit(x) for x in xs + xs]   # 6 batches over 2 lanes and 4 head buffers
+    pipe.drain()
     torch.cuda.synchronize()
     for i, (d, c, _, _) in enumerate(got):
         wd, wc = want[i % 3]

@@ -12,6 +12,14 @@ exactly the same computations here; only their scheduling changes:
 
 nms_image uses one workgroup per image (a few tens of CUs), so it fills CUs
 the forward leaves idle at its small 20x20 / 40x40 layers and tail ends.
+
+With several engines ("lanes", each its own workspace and captured graphs),
+consecutive batches' forwards also overlap: batch k runs on lane k % L, each
+lane on its own stream. The latency-bound 40x40 / 20x20 layers of one forward
+then share the chip with the other lane's layers instead of leaving CUs idle.
+All NMS calls stay on one stream in submission order (so a data-parallel
+gather is issued in the same order on every rank).
+
 Results are identical to the sequential order: every batch gets the full
 forward and the full NMS, on its own buffers.
 """
@@ -27,14 +35,21 @@ class DetectPipeline:
     data-parallel gather - and its return value is kept with the batch.
     """
 
-    def __init__(self, engine, batch, height, width, post=None, depth=2, nms_kwargs=None):
-        self.eng = engine
-        dev = engine.device
-        A = engine.num_anchors(height, width)
-        self.ys = [torch.empty((batch, 4 + engine.num_classes, A), dtype=engine.dtype, device=dev)
+    def __init__(self, engine, batch, height, width, post=None, depth=2, nms_kwargs=None, nms_on_lane=False):
+        # engine: one Engine, or a list of Engines with the same weights (forward lanes)
+        self.engs = list(engine) if isinstance(engine, (list, tuple)) else [engine]
+        self.eng = self.engs[0]
+        dev = self.eng.device
+        A = self.eng.num_anchors(height, width)
+        depth = max(depth, 2 * len(self.engs))
+        self.ys = [torch.empty((batch, 4 + self.eng.num_classes, A), dtype=self.eng.dtype, device=dev)
                    for _ in range(depth)]
         self.free = [None] * depth          # NMS-done event of the batch last held by each buffer
-        self.nms_stream = torch.cuda.Stream(device=dev)
+        # nms_on_lane: each batch's NMS follows its forward on the lane's stream (one
+        # stream fewer: the HIP runtime maps streams onto GPU_MAX_HW_QUEUES = 4 queues)
+        self.nms_stream = None if nms_on_lane else torch.cuda.Stream(device=dev)
+        # lane 0 runs on the caller's stream, the others on streams of their own
+        self.lane_streams = [None] + [torch.cuda.Stream(device=dev) for _ in self.engs[1:]]
         self.post = post
         self.nms_kwargs = nms_kwargs or {}
         self.k = 0
@@ -42,19 +57,29 @@ class DetectPipeline:
     def submit(self, x):
         main = torch.cuda.current_stream(self.eng.device)
         i = self.k % len(self.ys)
+        lane = self.k % len(self.engs)
         self.k += 1
         y = self.ys[i]
+        fs = main
+        if self.lane_streams[lane] is not None:
+            fs = self.lane_streams[lane]
+            ready = torch.cuda.Event()   # x (and anything else the caller queued) is ready
+            ready.record(main)
+            fs.wait_event(ready)
+            x.record_stream(fs)
         if self.free[i] is not None:
-            main.wait_event(self.free[i])
-        self.eng.forward(x, out=y)
-        fwd_done = torch.cuda.Event()
-        fwd_done.record(main)
-        with torch.cuda.stream(self.nms_stream):
-            self.nms_stream.wait_event(fwd_done)
+            fs.wait_event(self.free[i])
+        with torch.cuda.stream(fs):
+            self.engs[lane].forward(x, out=y)
+            fwd_done = torch.cuda.Event()
+            fwd_done.record(fs)
+        ns = self.nms_stream if self.nms_stream is not None else fs
+        with torch.cuda.stream(ns):
+            ns.wait_event(fwd_done)
             dets, counts = nms(y, **self.nms_kwargs)
             extra = self.post(dets, counts) if self.post is not None else None
             done = torch.cuda.Event()
-            done.record(self.nms_stream)
+            done.record(ns)
         self.free[i] = done
         # the results were allocated on the NMS stream; the caller reads them after `done`
         return dets, counts, extra, done
@@ -62,6 +87,9 @@ class DetectPipeline:
     def drain(self):
         """Make the caller's stream wait for every NMS in flight."""
         main = torch.cuda.current_stream(self.eng.device)
+        if len(self.engs) > 1:   # forwards still running on the lane streams
+            for fs in self.lane_streams[1:]:
+                main.wait_stream(fs)
         for e in self.free:
             if e is not None:
                 main.wait_event(e)
