@@ -1,7 +1,7 @@
 #!/bin/bash
 # Sweep forward lanes x segment split x HW queues for bench.py (v11_n b32 bf16).
 set -o pipefail
-O=gpurun_out/lanes3
+O=gpurun_out/lanes4
 mkdir -p $O
 run() {   # name, then KEY=VAL env settings, then bench args
     local n=$1; shift
@@ -9,10 +9,8 @@ run() {   # name, then KEY=VAL env settings, then bench args
     env "${envs[@]}" timeout -k 10 300 python bench.py --no-cpu-baseline --no-roofline --steps 40 "$@" > $O/$n.json 2> $O/$n.err || { tail -20 $O/$n.err; exit 1; }
     python -c "import json;d=json.load(open('$O/$n.json'));print('$n', d['value'], d['ms_per_step'])"
 }
-run l3_hs0 YH_HEADSPLIT=0 --lanes 3
-run l3_hs0_nl YH_HEADSPLIT=0 --lanes 3 --nms-on-lane
-run l4_hs0_nl YH_HEADSPLIT=0 --lanes 4 --nms-on-lane
-run l2_hs0_nl YH_HEADSPLIT=0 --lanes 2 --nms-on-lane
-run l4_hs0 YH_HEADSPLIT=0 --lanes 4
-run l2_hs1_nl YH_HEADSPLIT=1 --lanes 2 --nms-on-lane
-run l3_hs0_b YH_HEADSPLIT=0 --lanes 3
+run l3 --lanes 3
+run l3_ks0 YH_KSPLIT=0 --lanes 3
+run l3_direct YH_CONV=4 --lanes 3
+run l3_gemm YH_CONV=0 --lanes 3
+run l3_b2 --lanes 3
