@@ -893,7 +893,7 @@ __global__ __launch_bounds__(DIRECT_NT, 2) void conv_direct(const ConvArgs p) {
                     if (p.act == ACT_SILU) x = silu<T>(x);
                     v[e] = x;
                 }
-                if constexpr (RUN >= 8) {
+                if constexpr (RUN % 8 == 0) {
 #pragma unroll
                     for (int c8 = 0; c8 < RUN / 8; ++c8) {
                         if (co + c8 * 8 >= p.Cout) break;
@@ -909,15 +909,20 @@ __global__ __launch_bounds__(DIRECT_NT, 2) void conv_direct(const ConvArgs p) {
                         st_chunk(out + (long long)m * p.ldo + co + c8 * 8, f_to_chunk<T>(f));
                     }
                 } else {
-                    // RUN == 4: 8-byte store
-                    T o[4];
+                    // RUN = 4 or 20 (NTL 1 / 5): 8-byte stores, 8-byte aligned (co = n0 + q * RUN)
 #pragma unroll
-                    for (int e = 0; e < 4; ++e) {
-                        float x = fromf_round<T>(v[e]);
-                        if (res) x += tof(res[(long long)m * p.ldr + co + e]);
-                        o[e] = fromf<T>(x);
+                    for (int c4 = 0; c4 < RUN / 4; ++c4) {
+                        if (co + c4 * 4 >= p.Cout) break;
+                        T o[4];
+#pragma unroll
+                        for (int e = 0; e < 4; ++e) {
+                            float x = fromf_round<T>(v[c4 * 4 + e]);
+                            if (res) x += tof(res[(long long)m * p.ldr + co + c4 * 4 + e]);
+                            o[e] = fromf<T>(x);
+                        }
+                        *reinterpret_cast<uint2*>(out + (long long)m * p.ldo + co + c4 * 4) =
+                            *reinterpret_cast<const uint2*>(o);
                     }
-                    *reinterpret_cast<uint2*>(out + (long long)m * p.ldo + co) = *reinterpret_cast<const uint2*>(o);
                 }
             }
         }
@@ -950,8 +955,11 @@ int launch_direct_t(const ConvArgs& a, int lds, int S, hipStream_t s) {
 bool direct_plan(const ConvArgs& a, int* ntl_out, int* lds_out) {
     const bool k1 = a.KH == 1 && a.KW == 1 && a.stride == 1 && a.pad == 0;
     if (!k1 && (a.c1 != 0 || a.up0 != 0)) return false;
-    int ntl = a.Cout <= 16 ? 1 : a.Cout <= 32 ? 2 : 4;
+    // 80 couts (the v11_n class branch, c3 = 80) as one 5-tile slice: two 64-wide slices
+    // would read the input twice and spend 3/8 of their MFMAs on padding
+    int ntl = a.Cout <= 16 ? 1 : a.Cout <= 32 ? 2 : a.Cout == 80 ? 5 : 4;
     auto lds_of = [&](int n) { return n * 16 * (a.Kp * 2 + 16) + (a.Kp / 8 + 32) * 4; };
+    if (ntl == 5 && lds_of(5) > DIRECT_LDS_CAP) ntl = 4;
     while (ntl > 1 && lds_of(ntl) > DIRECT_LDS_CAP) ntl >>= 1;
     if (lds_of(ntl) > DIRECT_LDS_CAP) return false;
     if (ntl_out) *ntl_out = ntl;
@@ -976,6 +984,9 @@ int launch_direct(const ConvArgs& a, hipStream_t s) {
     switch (ntl) {
         case 1: YH_DIR(1)
         case 2: YH_DIR(2)
+        case 5:   // 1x1: 2 k-steps in flight keeps 4 waves/SIMD (D = 4 needs 132 VGPRs)
+            if (k1) return launch_direct_t<T, 5, 2, 0, 2>(a, lds, S, s);
+            YH_DIR(5)
         default: YH_DIR(4)
     }
 #undef YH_DIR
