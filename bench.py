@@ -148,8 +148,9 @@ def cpu_baseline(args, min_seconds=10.0, max_seconds=30.0):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=5)
+    # 50 steps: with 3 lanes the pipeline's fill and drain are a few % of a 20-step run
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--variant", default="n")
     ap.add_argument("--size", type=int, default=640)
     ap.add_argument("--batch", type=int, default=32, help="images per GPU per step")

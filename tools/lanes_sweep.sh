@@ -1,7 +1,7 @@
 #!/bin/bash
 # Sweep forward lanes x segment split x HW queues for bench.py (v11_n b32 bf16).
 set -o pipefail
-O=gpurun_out/lanes4
+O=gpurun_out/lanes5
 mkdir -p $O
 run() {   # name, then KEY=VAL env settings, then bench args
     local n=$1; shift
@@ -9,8 +9,8 @@ run() {   # name, then KEY=VAL env settings, then bench args
     env "${envs[@]}" timeout -k 10 300 python bench.py --no-cpu-baseline --no-roofline --steps 40 "$@" > $O/$n.json 2> $O/$n.err || { tail -20 $O/$n.err; exit 1; }
     python -c "import json;d=json.load(open('$O/$n.json'));print('$n', d['value'], d['ms_per_step'])"
 }
-run l3 --lanes 3
-run l3_ks0 YH_KSPLIT=0 --lanes 3
-run l3_direct YH_CONV=4 --lanes 3
-run l3_gemm YH_CONV=0 --lanes 3
-run l3_b2 --lanes 3
+run t0 --lanes 3
+run t3 YH_TUNE_TPUT=3 --lanes 3
+run t2 YH_TUNE_TPUT=2 --lanes 3
+run t0b --lanes 3
+run t3b YH_TUNE_TPUT=3 --lanes 3
