@@ -21,6 +21,25 @@ __global__ __launch_bounds__(256) void k_copy(const uint4* in, uint4* out, int l
     out[px * ldo8 + c] = v;
 }
 
+// 4 chunks per thread, all loads issued before the stores (more bytes in flight per wave)
+__global__ __launch_bounds__(256) void k_copy4(const uint4* in, uint4* out, int ldo8) {
+    const long long npx = (long long)B * H * W;
+    const long long n = npx * (COUT / 8);
+    const long long t0 = ((long long)blockIdx.x * 256) * 4 + threadIdx.x;
+    uint4 v[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+        const long long t = t0 + u * 256;
+        v[u] = t < n ? in[(t / (COUT / 8)) * (CIN / 8) + t % (COUT / 8)] : make_uint4(0, 0, 0, 0);
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+        const long long t = t0 + u * 256;
+        v[u].x ^= 0x5a5a5a5au;
+        if (t < n) out[(t / (COUT / 8)) * ldo8 + t % (COUT / 8)] = v[u];
+    }
+}
+
 int main() {
     const long long npx = (long long)B * H * W;
     uint4 *in, *out;
@@ -46,6 +65,15 @@ int main() {
         const double us = ms * 1e3 / reps;
         printf("ldo %2d ch: %7.2f us  %6.0f GB/s (64 B read + 64 B written per pixel, %.1f MB)\n", ldo, us,
                bytes / us / 1e3, bytes / 1e6);
+        const dim3 grid4((unsigned)((nthr + 1023) / 1024));
+        for (int r = 0; r < 3; ++r) hipLaunchKernelGGL(k_copy4, grid4, dim3(256), 0, 0, in, out, ldo / 8);
+        (void)hipEventRecord(e0, 0);
+        for (int r = 0; r < reps; ++r) hipLaunchKernelGGL(k_copy4, grid4, dim3(256), 0, 0, in, out, ldo / 8);
+        (void)hipEventRecord(e1, 0);
+        (void)hipEventSynchronize(e1);
+        (void)hipEventElapsedTime(&ms, e0, e1);
+        const double us4 = ms * 1e3 / reps;
+        printf("ldo %2d ch, 4 chunks/thread: %7.2f us  %6.0f GB/s\n", ldo, us4, bytes / us4 / 1e3);
     }
     (void)hipFree(in);
     (void)hipFree(out);
