@@ -16,6 +16,7 @@
  *                       (nets/nn.py:255-270), DFL (nets/nn.py:222-225) and make_anchors (utils/util.py:85-96)
  *   yh_forward_u8       main.py:265-267     uint8 -> dtype, / 255 preprocessing fused into yh_forward's stem
  *   yh_nms              utils/util.py:123-169 non_max_suppression (+ torchvision.ops.nms, util.py:162)
+ *   yh_nms_host         the same for head outputs on the CPU device (main.py:20 device fallback)
  *
  * Conventions
  *   - Every function returns 0 on success and a negative YH_E* code on failure;
@@ -40,7 +41,7 @@
 extern "C" {
 #endif
 
-#define YH_ABI_VERSION 1
+#define YH_ABI_VERSION 2
 
 /* status codes */
 #define YH_OK 0
@@ -144,6 +145,15 @@ int yh_nms(int dtype, const void* y, int batch, int num_classes, int anchors,
            float max_wh, void* workspace, size_t workspace_bytes,
            float* dets, int* counts, void* stream);
 
+/* The same NMS on the host CPU for a head output in HOST memory (the reference's
+ * CPU device path, main.py:20): identical candidate / order / suppression rules,
+ * torchvision's CPU loop in float32. dets (batch, max_det, 6) and counts (batch)
+ * are host arrays; `threads` <= 0 uses every hardware thread (images in parallel).
+ * Synchronous. */
+int yh_nms_host(int dtype, const void* y, int batch, int num_classes, int anchors,
+                float conf_threshold, double iou_threshold, int max_det, int max_nms,
+                float max_wh, float* dets, int* counts, int threads);
+
 /* Per-op instrumentation (bench / roofline). With profiling enabled,
  * yh_forward launches the ops eagerly with a HIP event pair around each op on
  * the caller's stream, synchronises at the end and accumulates per-op elapsed
@@ -181,22 +191,13 @@ int yh_op_kernel(const yh_handle* h, int index, int batch, int height, int width
 int yh_force_conv_kernel(yh_handle* h, int kernel);
 
 /* Launch units of the forward at (batch, height, width), known after the first
- * yh_forward at that shape: a unit is one op's kernel(s), or a run of ops of the
- * 40x40 / 20x20 levels fused into one level-program launch (is_level = 1).
+ * yh_forward at that shape: a unit is one op's kernel (is_level is always 0; the
+ * fused level programs of ABI 1 are gone).
  * yh_unit_count returns the count (YH_ESTATE before that forward). With
  * yh_profile_enable, ms_total / calls accumulate per unit. */
 int yh_unit_count(const yh_handle* h, int batch, int height, int width);
 int yh_unit_info(const yh_handle* h, int index, int batch, int height, int width, int* first_op,
                  int* num_ops, int* is_level, double* ms_total, int* calls);
-
-/* Fuse the 40x40 / 20x20 levels into level programs (16-bit handles; default
- * off, or on with YH_LEVEL=1; outputs are bit-identical either way). Drops
- * graphs and tuning. */
-int yh_set_level_fusion(yh_handle* h, int enable);
-
-/* 0 when no level-program cluster barrier has timed out on this handle, 1 if
- * one has (results of that forward are invalid), <0 on error. Synchronous. */
-int yh_level_status(const yh_handle* h);
 
 #ifdef __cplusplus
 }

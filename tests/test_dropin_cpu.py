@@ -85,10 +85,17 @@ def test_wh2xy():
     assert wh2xy(b).tolist() == [[8.0, 17.0, 12.0, 23.0]]
 
 
-def test_cpu_nms_is_not_silently_emulated():
+def test_cpu_nms_runs_the_native_host_path():
+    """main.py:20 falls back to the CPU device: the drop-in NMS runs yh_nms_host (C++),
+    returns the reference's float32 rows (util.py:148 promotes through j.float())."""
     from utils.util import non_max_suppression
-    with pytest.raises(NotImplementedError):
-        non_max_suppression(torch.zeros(1, 84, 10))
+    from yolo_hip import synth
+    y = torch.stack([synth.synth_head_output(8400, 80, seed=1, mode="typical")])
+    for dt in (torch.float32, torch.float16, torch.bfloat16):
+        out = non_max_suppression(y.to(dt))
+        assert len(out) == 1 and out[0].dtype == torch.float32 and out[0].shape[1] == 6 and out[0].shape[0] > 0
+    empty = non_max_suppression(torch.zeros(2, 84, 10))
+    assert [tuple(o.shape) for o in empty] == [(0, 6), (0, 6)] and empty[0].dtype == torch.float32
 
 
 def test_training_mode_returns_level_maps():

@@ -1,11 +1,13 @@
-"""Every dense-conv kernel implementation gives bit-identical forwards. Marked gpu.
+"""Every conv_mx plan gives bit-identical forwards. Marked gpu.
 
-The per-shape autotuner (csrc/engine.cpp ensure_tuned) may pick any of
-conv_gemm2 (3 tile shapes), conv_stream (2-, 4- and 8-slot rings),
-conv_direct and conv_tiny per layer. That is only valid because they all accumulate K in the
-same order (32-deep MFMA steps, increasing k): this test forces each one on
-every layer that supports it and requires the exact same head output as the
-reference kernel (conv_gemm2), which the forward parity tests pin to the oracle.
+The per-shape autotuner (csrc/engine.cpp ensure_tuned) picks, per layer, one of
+the layer's conv_mx candidate plans (csrc/conv_mx.hip: conv_mx with staged
+weights, conv_mxr with resident weights; different tile shapes, cout slices and
+16-channel blocks per stage). That is only valid because every plan follows one
+reduction order (conv_mx.h: for each 16-channel block, for each tap, one
+32x32x16 MFMA step): this test forces candidate k on every layer (clamped to the
+layer's last candidate) and requires the exact same head output for every k and
+for the tuned choice. The forward parity tests pin that output to the oracle.
 """
 import pytest
 import torch
@@ -14,29 +16,29 @@ from yolo_hip import synth
 
 pytestmark = pytest.mark.gpu
 
-KERNELS = ["gemm", "gemm64", "gemm128", "stream", "direct", "stream4", "stream8", "tiny"]
 
-
-@pytest.mark.parametrize("dtype,batch", [(torch.bfloat16, 32), (torch.float16, 4)])
-def test_all_conv_kernels_bit_identical(gpu, dtype, batch):
+@pytest.mark.parametrize("variant,dtype,batch,size", [("n", torch.bfloat16, 32, 640), ("n", torch.float16, 4, 640),
+                                                      ("s", torch.float16, 8, 640)])
+def test_all_conv_plans_bit_identical(gpu, variant, dtype, batch, size):
     from nets import nn
     from yolo_hip.engine import Engine
     torch.manual_seed(0)
-    model = nn.yolo_v11_n(80)
+    model = getattr(nn, f"yolo_v11_{variant}")(80)
     model.load_state_dict(synth.synth_state_dict(model.state_dict(), seed=0))
     model.eval()
     eng = Engine(*model._yh_arch, gpu, dtype)
     eng.load_module(model)
-    x = synth.synth_scenes(batch, 640, 640, seed=11).to(gpu, dtype)
-    outs = {}
-    for k, name in enumerate(KERNELS):
+    x = synth.synth_scenes(batch, size, size, seed=11).to(gpu, dtype)
+    outs, names = {}, set()
+    for k in range(8):
         eng.force_conv_kernel(k)
-        outs[name] = eng.forward(x).clone()
-        used = {o["kernel"] for o in eng.ops(batch, 640, 640) if o["cls"] in ("conv1x1", "conv3x3")}
-        assert name in used, f"kernel {name} ran on no layer ({used})"
+        outs[k] = eng.forward(x).clone()
+        names |= {o["kernel"] for o in eng.ops(batch, size, size) if o["cls"] in ("conv1x1", "conv3x3")}
     eng.force_conv_kernel(-1)
     outs["tuned"] = eng.forward(x).clone()
-    ref = outs["gemm"]
+    names |= {o["kernel"] for o in eng.ops(batch, size, size) if o["cls"] in ("conv1x1", "conv3x3")}
+    assert any(n.startswith("mxr") for n in names) and any(n.startswith("mx_") for n in names), names
+    ref = outs[0]
     assert torch.isfinite(ref.float()).all()
-    for name, y in outs.items():
-        assert torch.equal(y, ref), f"{name}: {(y.float() - ref.float()).abs().max().item()} max diff vs gemm"
+    for k, y in outs.items():
+        assert torch.equal(y, ref), f"plan {k}: {(y.float() - ref.float()).abs().max().item()} max diff vs plan 0"

@@ -96,50 +96,6 @@ struct NmsArgs {
     unsigned long long* trace;  // optional [B][16] phase timestamps (s_memrealtime), nullptr = off
 };
 
-// Level program (csrc/level.hip): a run of consecutive ops whose outputs live on
-// the 40x40 / 20x20 pyramid levels, executed by ONE persistent launch. Each image
-// is owned by a cluster of G workgroups that split every op's output pixels
-// (attention: query tiles) and meet at a cluster barrier between ops; inside the
-// launch activations move only through sc1 stores / sc1 loads (L1 bypass), and
-// no tensor region is rewritten after another workgroup has read it.
-enum LevelOpKind { LOP_CONV = 0, LOP_DW = 1, LOP_POOL = 2, LOP_ATTN = 3 };
-struct LevelOp {
-    int kind;
-    int sync;        // 1: the cluster barrier must precede this op (it reads, across the
-                     //    pixel partition, data written since the last barrier)
-    int nt;          // LOP_CONV: 16-cout MFMA tiles per wave work unit (1, 2 or 4)
-    int step;        // LOP_POOL: pool i reads concat slice i, writes slice i+1
-    int patch;       // LOP_CONV: 1 = stage the workgroup's input rows (+halo) in LDS
-    int pstride;     //   bytes per patch pixel (Cin_p * 2 + 16: conflict-free b128 reads)
-    int wp;          //   patch row width in pixels (Wi + 2 * pad, zero border)
-    int band;        //   16-pixel tiles per patch band (LDS budget)
-    int wn;          //   waves along the cout chunks (the other LP_W / wn split the band's pixel tiles)
-    int kcs;         //   32-deep k steps per LDS weight chunk (double-buffered, shared by all waves)
-    int wpitch;      //   bytes per weight row in a chunk (kcs * 64 + 16)
-    int woff;        //   LDS byte offset of the weight buffers (after the patch region)
-    int pc;          //   cluster split: pc cout-chunk ranges x (G / pc) pixel ranges
-    int wcount;      //   elements of the packed weights, floats of the bias (bounds checks)
-    int bcount;
-    ConvArgs c;      // LOP_CONV (ktab padded, see engine)
-    DwArgs d;        // LOP_DW
-    PoolArgs pl;     // LOP_POOL
-    AttnArgs at;     // LOP_ATTN (positional dwconv pe(v) fused)
-};
-struct LevelArgs {
-    const LevelOp* ops; int nops;
-    int B, G, NC;      // images, workgroups per cluster, clusters (grid = G * NC)
-    const void* base;  // workspace base: activations are addressed by 32-bit byte offsets from it
-    unsigned* bar;     // [NC][64] barrier words (count at +0, generation at +32), zero-initialised,
-                       // then [NC][32] XCC ids of the members
-    int* err;          // set to 1 when a cluster barrier times out
-    int lds_patch;     // dynamic LDS bytes for conv input patches
-    int skip;          // debug: bit k set = skip ops of LevelOpKind k (timing experiments only)
-    unsigned long long* trace;  // debug: [nops][8] s_memrealtime stamps of block 0 per op
-    int plain_ok;      // allow plain (L2-resident) activation stores in same-XCD clusters
-};
-int launch_level(int dtype, const LevelArgs& a, hipStream_t s);
-int level_ktab_max();
-
 // Dense-conv kernels (16-bit types; F32 always runs conv_gemm). All of them
 // accumulate the K reduction in the same order (32-deep MFMA steps, increasing
 // k), so they produce bit-identical outputs and the engine may pick per layer.

@@ -20,6 +20,7 @@
 #include <vector>
 
 #include "common.h"
+#include "conv_mx.h"
 #include "yolo_hip.h"
 
 // YH_SEGV_BT=1 (debugging): print a native backtrace on SIGSEGV before the
@@ -33,7 +34,6 @@ static void segv_bt(int sig) {
     raise(sig);
 }
 
-static unsigned long long* level_trace_ptr = nullptr;   // yh_debug_level_trace
 
 namespace yh {
 
@@ -108,6 +108,8 @@ struct ConvDesc {
     void* w_dev = nullptr;
     float* b_dev = nullptr;
     int* ktab_dev = nullptr;
+    std::vector<int> phys2log;                  // dense: physical input channel -> logical (-1 = pad)
+    std::map<std::string, void*> mx_w;          // 16-bit dense: packed weights per conv_mx layout
 };
 
 struct Op {
@@ -147,7 +149,6 @@ struct Net {
     void* zero_dev = nullptr;     // 256 zero bytes: source of padded conv taps
     bool use_graph = true;
     std::map<GraphKey, hipGraphExec_t> graphs;
-    std::map<GraphKey, std::vector<hipEvent_t>> graph_events;   // events a capture used: live as long as its exec
     hipStream_t cap_stream = nullptr;
     bool profile = false;
     std::vector<double> prof_ms;     // per launch unit of the profiled shape
@@ -158,20 +159,19 @@ struct Net {
     // per-shape choice of dense-conv kernel for every op (ConvKernel; CONV_GEMM for
     // non-conv ops): timed once per (B, H, W) on the caller's stream, or forced by
     // YH_CONV=<kernel id>
-    std::map<GraphKey, std::vector<int>> conv_kern;
-    const std::vector<int>* cur_kern = nullptr;
-    int force_kern = -1;   // yh_force_conv_kernel (testing); -1 = autotune / YH_CONV
-    // launch units of the forward at the current shape: a single op, or a run of
-    // ops fused into one level-program launch (csrc/level.hip)
-    struct Unit { int first, last; bool level; int lop_off, lop_cnt; };
-    struct Plan { std::vector<Unit> units; LevelOp* lops_dev = nullptr; int NC = 0, G = 0; std::vector<int> lds; };
+    // 16-bit dense convs: the conv_mx plan chosen for every op at a shape (all plans of a
+    // layer are bit-identical, the choice only changes speed), timed once per (B, H, W)
+    // on the caller's stream or forced by yh_force_conv_kernel / YH_CONV=<candidate>
+    struct MxChoice { MxPlan plan; const char* w = nullptr; std::string name; };
+    std::map<GraphKey, std::vector<MxChoice>> conv_kern;
+    const std::vector<MxChoice>* cur_kern = nullptr;
+    int force_kern = -1;   // candidate index (testing); -1 = autotune
+    int num_cus = 0;
+    // launch units of the forward at the current shape (one op each)
+    struct Unit { int first, last; bool level; };
+    struct Plan { std::vector<Unit> units; };
     std::map<GraphKey, Plan> plans;
     const Plan* cur_plan = nullptr;
-    // level programs are opt-in (YH_LEVEL=1 or yh_set_level_fusion) until they beat
-    // the per-layer kernels
-    bool use_level = [] { const char* e = getenv("YH_LEVEL"); return e && atoi(e) != 0; }();
-    unsigned* bar_dev = nullptr;   // [32][64] cluster barrier words
-    int* lerr_dev = nullptr;       // level-program barrier timeout flag
 
     // ---------------------------------------------------------- builder
     int tensor(int level, int C) {
@@ -240,7 +240,7 @@ struct Net {
     // CSPModule / C3k (nn.py:52-63)
     // The residual chain a -> a' -> a'' runs through fresh tensors (not in place)
     // so that no region is rewritten after a 3x3 conv of another workgroup read
-    // it (the level program's hand-off rule, csrc/level.hip); the last link
+    // it; the last link
     // writes into the concat buffer.
     void cspmodule(const std::string& p, View x, int in_ch, int out_ch, View out, int level) {
         const int h = out_ch / 2;
@@ -468,6 +468,7 @@ struct Net {
                 lo += s.first;
                 ph += s.second;
             }
+            d.phys2log = phys2log;
             const size_t per = (size_t)d.cin * d.k * d.k;
             for (int kh = 0; kh < d.k; ++kh)
                 for (int kw = 0; kw < d.k; ++kw)
@@ -513,6 +514,8 @@ struct Net {
     }
 
     static void free_conv(ConvDesc& d) {
+        for (auto& kv : d.mx_w) (void)hipFree(kv.second);
+        d.mx_w.clear();
         if (d.w_dev) (void)hipFree(d.w_dev);
         if (d.b_dev) (void)hipFree(d.b_dev);
         if (d.ktab_dev) (void)hipFree(d.ktab_dev);
@@ -576,9 +579,6 @@ struct Net {
         }
         for (auto& kv : graphs) (void)hipGraphExecDestroy(kv.second);
         graphs.clear();
-        for (auto& kv : graph_events)
-            for (auto e : kv.second) (void)hipEventDestroy(e);
-        graph_events.clear();
         free_plans();
     }
 
@@ -663,59 +663,115 @@ struct Net {
         return a;
     }
 
-    // Pick the dense-conv kernel of every conv op for this shape: one plain forward
-    // (realistic activations in the workspace), then each candidate kernel of each
-    // conv timed over 3 launches after a warm-up launch. The candidates produce
-    // bit-identical outputs, so the choice only changes speed. Runs outside any
-    // graph capture; the caller's next forward recomputes every activation.
+    // ---------------------------------------------------------- conv_mx (16-bit dense convs)
+    MxShape mx_shape(const ConvArgs& a, int B) const {
+        MxShape sh{};
+        sh.ks = a.KH; sh.s = a.stride; sh.cin = a.Cin; sh.cout = a.Cout;
+        sh.Hi = a.Hi; sh.Wi = a.Wi; sh.Ho = a.Ho; sh.Wo = a.Wo; sh.B = B;
+        sh.c0 = a.c1 ? a.c0 : a.Cin; sh.c1 = a.c1; sh.up0 = a.up0; sh.up1 = a.up1;
+        return sh;
+    }
+    static std::string mx_name(const MxPlan& p) {
+        char b[96];
+        snprintf(b, sizeof(b), "%s_na%d_mb%d_w%dx%d_ncb%d_t%dx%d", p.cfg.kind ? "mxr" : "mx", p.cfg.na, p.cfg.mb, p.cfg.wn,
+                 p.cfg.wm, p.cfg.ncb, p.TH, p.TW);
+        return b;
+    }
+    // packed weights of conv `ci` in the layout of plan `p` (cached per layout)
+    const char* mx_weights(int ci, const MxPlan& p, const MxShape& sh) {
+        ConvDesc& d = convs[ci];
+        char k[96];
+        snprintf(k, sizeof(k), "%d/%d/%d/%d/%d/%d/%d/%d", p.cfg.kind, p.cfg.ks, p.cfg.na, p.cfg.wn, p.cfg.ncb, p.nst,
+                 p.nslices, p.wstage);
+        auto it = d.mx_w.find(k);
+        if (it != d.mx_w.end()) return (const char*)it->second;
+        require(d.loaded, "weights of " + d.name + " not loaded", YH_ESTATE);
+        const std::vector<uint16_t> pk = mx_pack(p, sh, d.wf.data(), d.cin, d.phys2log, dtype == BF16, d.cout);
+        void* dev = nullptr;
+        HIPCHECK(hipMalloc(&dev, pk.size() * 2));
+        HIPCHECK(hipMemcpy(dev, pk.data(), pk.size() * 2, hipMemcpyHostToDevice));
+        d.mx_w.emplace(k, dev);
+        return (const char*)dev;
+    }
+    int launch_mx_op(const Op& op, const MxPlan& pl, int B, int H, int W, hipStream_t s) {
+        ConvArgs a{};
+        int BM, BN;
+        conv_args(op, B, H, W, a, BM, BN);
+        const MxShape sh = mx_shape(a, B);
+        MxArgs m{};
+        mx_fill_args(pl, sh, m);
+        m.in0 = (const char*)a.in0;
+        m.in1 = a.c1 ? (const char*)a.in1 : nullptr;
+        m.ldc0 = a.ldc0; m.ldc1 = a.ldc1;
+        m.hs0 = a.h0; m.ws0 = a.w0; m.hs1 = a.h1; m.ws1 = a.w1;
+        m.w = mx_weights(op.conv, pl, sh);
+        m.bias = a.bias;
+        m.out = (char*)a.out; m.ldo = a.ldo;
+        m.res = (const char*)a.res; m.ldr = a.ldr;
+        m.act = a.act;
+        m.zero = (const char*)zero_dev;
+        return launch_mx(dtype, pl, m, s);
+    }
+
+    // Pick the conv_mx plan of every dense conv for this shape: one plain forward with
+    // each layer's default plan (realistic activations in the workspace), then every
+    // candidate plan of every layer timed over 3 launches after a warm-up launch. The
+    // candidates are bit-identical (one reduction order), so the choice only changes
+    // speed. Runs outside any graph capture; the next forward recomputes everything.
     void ensure_tuned(int B, int H, int W, hipStream_t s) {
+        if (dtype == F32) return;   // conv_gemm only
         const GraphKey key{B, H, W};
         auto it = conv_kern.find(key);
         if (it != conv_kern.end()) { cur_kern = &it->second; return; }
-        std::vector<int> ch(ops.size(), CONV_GEMM);
+        if (!num_cus) HIPCHECK(hipDeviceGetAttribute(&num_cus, hipDeviceAttributeMultiprocessorCount, device));
         static const int env_forced = [] { const char* e = getenv("YH_CONV"); return e ? atoi(e) : -1; }();
         const int forced = force_kern >= 0 ? force_kern : env_forced;
         static const bool tune_log = getenv("YH_TUNE_LOG") != nullptr;
-        if (dtype != F32) {
-            cur_kern = nullptr;
-            std::vector<ConvArgs> args(ops.size());
-            std::vector<int> bms(ops.size()), bns(ops.size());
-            for (size_t i = 0; i < ops.size(); ++i)
-                if (ops[i].kind == OP_CONV) conv_args(ops[i], B, H, W, args[i], bms[i], bns[i]);
-            if (forced >= 0) {
-                for (size_t i = 0; i < ops.size(); ++i)
-                    if (ops[i].kind == OP_CONV && conv_kernel_ok(dtype, forced, args[i])) ch[i] = forced;
-            } else {
-                run_ops(B, H, W, s);
-                hipEvent_t e0, e1;
-                HIPCHECK(hipEventCreate(&e0));
-                HIPCHECK(hipEventCreate(&e1));
-                std::vector<char> fused(ops.size(), 0);
-                if (cur_plan)
-                    for (auto& u : cur_plan->units)
-                        if (u.level) for (int k = u.first; k < u.last; ++k) fused[k] = 1;
-                for (size_t i = 0; i < ops.size(); ++i) {
-                    if (ops[i].kind != OP_CONV || fused[i] || args[i].ks > 1) continue;   // ks: fixed by rule
-                    float best = 1e30f;
-                    for (int k = 0; k < CONV_NKERNELS; ++k) {
-                        if (!conv_kernel_ok(dtype, k, args[i])) continue;
-                        int rc = launch_conv(dtype, k, bms[i], bns[i], args[i], s);
-                        HIPCHECK(hipEventRecord(e0, s));
-                        for (int r = 0; r < 3 && rc == 0; ++r) rc = launch_conv(dtype, k, bms[i], bns[i], args[i], s);
-                        HIPCHECK(hipEventRecord(e1, s));
-                        HIPCHECK(hipEventSynchronize(e1));
-                        if (rc != 0) throw Fail(YH_EHIP, "tuning launch of " + ops[i].label + " failed");
-                        float ms = 0.f;
-                        HIPCHECK(hipEventElapsedTime(&ms, e0, e1));
-                        if (tune_log) fprintf(stderr, "[yh tune] %-36s kernel %d  %8.2f us\n", ops[i].label.c_str(), k, ms * 1e3f / 3);
-                        if (ms < best) { best = ms; ch[i] = k; }
-                    }
+        std::vector<MxChoice> ch(ops.size());
+        std::vector<std::vector<MxPlan>> cands(ops.size());
+        for (size_t i = 0; i < ops.size(); ++i) {
+            if (ops[i].kind != OP_CONV) continue;
+            ConvArgs a{};
+            int BM, BN;
+            conv_args(ops[i], B, H, W, a, BM, BN);
+            cands[i] = mx_candidates(mx_shape(a, B), num_cus);
+            require(!cands[i].empty(), "no conv_mx plan for " + ops[i].label);
+            const int pick = forced >= 0 ? std::min(forced, (int)cands[i].size() - 1) : 0;
+            ch[i].plan = cands[i][pick];
+            ch[i].name = mx_name(ch[i].plan);
+        }
+        auto& slot = conv_kern[key];
+        slot = ch;
+        cur_kern = &slot;
+        if (forced >= 0) return;
+        run_ops(B, H, W, s);
+        hipEvent_t e0, e1;
+        HIPCHECK(hipEventCreate(&e0));
+        HIPCHECK(hipEventCreate(&e1));
+        for (size_t i = 0; i < ops.size(); ++i) {
+            if (ops[i].kind != OP_CONV || cands[i].size() < 2) continue;
+            float best = 1e30f;
+            for (const MxPlan& pl : cands[i]) {
+                int rc = launch_mx_op(ops[i], pl, B, H, W, s);
+                HIPCHECK(hipEventRecord(e0, s));
+                for (int r = 0; r < 3 && rc == 0; ++r) rc = launch_mx_op(ops[i], pl, B, H, W, s);
+                HIPCHECK(hipEventRecord(e1, s));
+                HIPCHECK(hipEventSynchronize(e1));
+                if (rc != 0) throw Fail(YH_EHIP, "tuning launch of " + ops[i].label + " failed");
+                float ms = 0.f;
+                HIPCHECK(hipEventElapsedTime(&ms, e0, e1));
+                if (tune_log)
+                    fprintf(stderr, "[yh tune] %-36s %-40s %8.2f us\n", ops[i].label.c_str(), mx_name(pl).c_str(),
+                            ms * 1e3f / 3);
+                if (ms < best) {
+                    best = ms;
+                    slot[i].plan = pl;
+                    slot[i].name = mx_name(pl);
                 }
-                (void)hipEventDestroy(e0);
-                (void)hipEventDestroy(e1);
             }
         }
-        cur_kern = &conv_kern.emplace(key, std::move(ch)).first->second;
+        (void)hipEventDestroy(e0);
+        (void)hipEventDestroy(e1);
     }
 
     void launch_op(size_t oi, int B, int H, int W, hipStream_t s) {
@@ -739,11 +795,15 @@ struct Net {
                 break;
             }
             case OP_CONV: {
+                if (dtype != F32) {
+                    require(cur_kern != nullptr, "conv plans not chosen", YH_ESTATE);
+                    rc = launch_mx_op(op, (*cur_kern)[oi].plan, B, H, W, s);
+                    break;
+                }
                 ConvArgs a{};
                 int BM, BN;
                 conv_args(op, B, H, W, a, BM, BN);
-                const int kern = cur_kern ? (*cur_kern)[oi] : CONV_GEMM;
-                rc = launch_conv(dtype, kern, BM, BN, a, s);
+                rc = launch_conv(dtype, CONV_GEMM, BM, BN, a, s);
                 break;
             }
             case OP_DW: rc = launch_dwconv(dtype, dw_args(op, B, H, W), s); break;
@@ -769,253 +829,9 @@ struct Net {
         if (rc != 0) throw Fail(YH_EHIP, "launch of " + op.label + " failed: " + hipGetErrorString((hipError_t)rc));
     }
 
-    // ---------------------------------------------------------- level program
-    int out_level(const Op& op) const {
-        if (op.kind == OP_DECODE) return 0;
-        return tensors[op.out.t].level;
-    }
-    bool level_eligible(const Op& op) const {
-        if (dtype == F32 || !use_level) return false;
-        // clusters of 8 workgroups only (>= 25 images per launch): larger clusters
-        // (small batches) faulted on the device and are not yet understood
-        if (level_G_ != 8) return false;
-        if (op.kind == OP_FIRST || op.kind == OP_DECODE) return false;
-        if (out_level(op) < 4) return false;
-        if (op.kind == OP_CONV && convs[op.conv].Kp / 8 > level_ktab_max()) return false;
-        return true;
-    }
-    // Reads that cross the pixel partition of the op's level (halo, stride,
-    // upsample, attention keys, pools) versus pixel-local ones (1x1 at the
-    // same level, residuals, depthwise centre excluded).
-    bool pixel_local(const Op& op) const {
-        if (op.kind != OP_CONV) return false;
-        const ConvDesc& d = convs[op.conv];
-        if (d.k != 1 || d.stride != 1) return false;
-        for (auto& sg : op.in)
-            if (sg.up || tensors[sg.v.t].level != tensors[op.out.t].level) return false;
-        return true;
-    }
-    // Hand-off rule of the level program: within one launch, no channel range of a
-    // tensor is written after a non-pixel-local read of it, and pixel-local
-    // in-place rewrites only touch tensors whose pixel rows fill whole 128-B lines.
-    bool segment_safe(int first, int last) const {
-        struct Rng { int t, c0, c1; };
-        std::vector<Rng> nonlocal, written;
-        auto overlap = [](const Rng& a, const Rng& b) { return a.t == b.t && a.c0 < b.c1 && b.c0 < a.c1; };
-        for (int i = first; i < last; ++i) {
-            const Op& op = ops[i];
-            std::vector<Rng> reads;
-            for (auto& sg : op.in) reads.push_back({sg.v.t, sg.v.coff, sg.v.coff + sg.v.C});
-            if (op.res.t >= 0 && op.has_res) reads.push_back({op.res.t, op.res.coff, op.res.coff + op.res.C});
-            const bool local = pixel_local(op);
-            std::vector<Rng> outs;
-            if (op.kind == OP_SPPF) {
-                // pool i reads slice i, writes slice i+1: writes never precede a read of themselves
-                const int C = op.out.C;
-                for (int k = 0; k < 3; ++k) {
-                    const Rng w{op.out.t, op.out.coff + (k + 1) * C, op.out.coff + (k + 2) * C};
-                    for (auto& r : nonlocal)
-                        if (overlap(w, r)) return false;
-                    nonlocal.push_back({op.out.t, op.out.coff + k * C, op.out.coff + (k + 1) * C});
-                    written.push_back(w);
-                }
-                continue;
-            }
-            for (auto& r : reads)
-                if (!local) nonlocal.push_back(r);
-            outs.push_back({op.out.t, op.out.coff, op.out.coff + op.out.C});
-            for (auto& w : outs) {
-                for (auto& r : nonlocal)
-                    if (overlap(w, r)) return false;
-                for (auto& r : written)
-                    if (overlap(w, r) && (tensors[w.t].C * es) % 128 != 0) return false;
-                written.push_back(w);
-            }
-        }
-        return true;
-    }
-    // LDS bytes of the largest input patch (rows of the workgroup's output pixels
-    // plus the conv's halo, zero border, all input channels) over the G members
-    static constexpr int LEVEL_PATCH_MAX = 112 * 1024;
-    // worst-case LDS bytes of a band of `tiles` 16-pixel tiles (any alignment)
-    static int band_bytes(const ConvArgs& c, int tiles) {
-        const int rows_out = (16 * tiles - 1 + c.Wo - 1) / c.Wo + 1;
-        const int rows_in = (rows_out - 1) * c.stride + c.KH;
-        return rows_in * (c.Wi + 2 * c.pad) * (c.Cin * 2 + 16) + 16;
-    }
-    // largest band (in tiles, <= a member's tile count) within the LDS budget; 0 = none fits
-    static int patch_band(const ConvArgs& c, int G) {
-        const int npt = (c.Ho * c.Wo + 15) / 16;
-        const int per = (npt + G - 1) / G;
-        int b = 0;
-        while (b < per && band_bytes(c, b + 1) <= LEVEL_PATCH_MAX) ++b;
-        return b;
-    }
-    static int patch_bytes(const ConvArgs& c, int band) { return band > 0 ? band_bytes(c, band) : 0; }
-    int G_ = 8;   // cluster size of the plan being built
-    int level_G_ = 8;
-    static constexpr int LEVEL_LDS_MAX = 120 * 1024;   // dynamic LDS of the level program (static: ~24 KB)
-    static constexpr int LEVEL_WBUF_MAX = 64 * 1024;   // both weight chunk buffers together
-    // Patch conv plan: cout chunk width nt, wave grid wn x (8 / wn), weight chunk
-    // depth kcs, band size (one block of <= 4 pixel tiles per wave and band) and the
-    // LDS layout [zero fragment | patch | weight chunk x 2]. patch = 0 if nothing fits.
-    void plan_patch_conv(LevelOp& L) const {
-        // Candidates: cout chunk width nt, cluster split pc (cout ranges) x G/pc (pixel
-        // ranges). Each is costed in memory round trips per workgroup (one per patch
-        // band, one per weight chunk of every band; ~1.4 us each under load) plus
-        // MFMA time; the cheapest that fits the LDS budget wins.
-        const ConvArgs& c = L.c;
-        const int nct = (c.Cout + 15) / 16;
-        const int nks = (c.K + 31) / 32;
-        const int npt = (c.Ho * c.Wo + 15) / 16;
-        double best = 1e30;
-        LevelOp bestL = L;
-        bestL.patch = 0;
-        for (int nt : {4, 2, 1}) {
-            if (nt > 1 && nct < nt) continue;
-            const int nchall = (nct + nt - 1) / nt;
-            for (int pc : {1, 2, 4, 8}) {
-                if (pc > G_ || G_ % pc || pc > nchall) continue;
-                const int nch = (nchall + pc - 1) / pc;           // chunks of the largest range
-                const int wn = nch >= 8 ? 8 : nch >= 4 ? 4 : nch >= 2 ? 2 : 1;
-                if (nch > wn) continue;                           // one cout chunk per wave column
-                const int wm = 8 / wn;
-                const int wrows = nch * 16 * nt;
-                int kcs = 1;
-                while (kcs < nks && 2 * wrows * ((kcs + 1) * 64 + 16) <= LEVEL_WBUF_MAX && wrows * (kcs + 1) * 4 <= 8 * 512)
-                    ++kcs;
-                if (2 * wrows * (kcs * 64 + 16) > LEVEL_WBUF_MAX || wrows * kcs * 4 > 8 * 512) continue;
-                const int wbytes = 2 * wrows * (kcs * 64 + 16);
-                const int pm = G_ / pc;
-                const int tiles = (npt + pm - 1) / pm;
-                int band = 0;
-                while (band < std::min(tiles, wm * 4) && band_bytes(c, band + 1) + 16 + wbytes <= LEVEL_LDS_MAX) ++band;
-                if (band == 0) continue;
-                const int bands = (tiles + band - 1) / band;
-                const int chunks = (nks + kcs - 1) / kcs;
-                const double mfma_us = (double)tiles * nch * nt * nks * 16 / 4 / 2.1e3;   // 4 SIMDs, ~2.1 GHz
-                const double cost = bands * (1 + chunks) * 1.4 + mfma_us;
-                if (cost < best - 1e-9) {
-                    best = cost;
-                    bestL = L;
-                    bestL.nt = nt; bestL.pc = pc; bestL.wn = wn; bestL.kcs = kcs; bestL.wpitch = kcs * 64 + 16;
-                    bestL.band = band; bestL.woff = (band_bytes(c, band) + 15) / 16 * 16; bestL.patch = 1;
-                }
-            }
-        }
-        L = bestL;
-        if (!L.patch) {
-            L.nt = nct >= 4 ? 4 : nct >= 2 ? 2 : 1;
-            L.pc = 1;
-        }
-    }
-    LevelOp level_op(const Op& op, int B, int H, int W, int sub) const {
-        LevelOp L;
-        std::memset(&L, 0, sizeof(L));
-        switch (op.kind) {
-            case OP_CONV: {
-                int BM, BN;
-                L.kind = LOP_CONV;
-                conv_args(op, B, H, W, L.c, BM, BN);
-                const int nct = (L.c.Cout + 15) / 16;
-                L.nt = nct >= 4 ? 4 : nct >= 2 ? 2 : 1;
-                L.pstride = L.c.Cin * 2 + 16;
-                L.wp = L.c.Wi + 2 * L.c.pad;
-                L.wcount = convs[op.conv].coutp_pad * convs[op.conv].Kp;
-                L.bcount = convs[op.conv].coutp_pad;
-                plan_patch_conv(L);
-                break;
-            }
-            case OP_DW: L.kind = LOP_DW; L.d = dw_args(op, B, H, W); break;
-            case OP_SPPF: L.kind = LOP_POOL; L.step = sub; L.pl = pool_args(op, B, H, W); break;
-            case OP_ATTN: L.kind = LOP_ATTN; L.at = attn_args(op, H, W); break;
-            default: throw Fail(YH_EINVAL, "op kind not supported by the level program");
-        }
-        return L;
-    }
-    // Which level ops need the cluster barrier before them: those reading data
-    // written since the last barrier other than their own pixels at their own
-    // level (3x3 / strided / upsampled / attention / pool / depthwise reads, or a
-    // 1x1 reading another level's partition). SPPF is three pool ops, each
-    // reading the previous one's output.
-    // A pixel-local read of data written since the last barrier is safe only if
-    // writer and reader split the image's pixels the same way (the G-way pixel
-    // partition: convs with pc == 1, depthwise, pools) at the same level.
-    // Host replay of the patch conv's index arithmetic for every member of a
-    // cluster: weight / bias / k-table reads inside their allocations, the patch
-    // and both weight buffers inside the planned LDS. Throws on a planning bug.
-    void validate_level_op(const LevelOp& L, int G) const {
-        if (L.kind != LOP_CONV || !L.patch) return;
-        const ConvArgs& c = L.c;
-        const int P = c.Ho * c.Wo, npt = (P + 15) / 16;
-        const int nchall = (c.Cout + 16 * L.nt - 1) / (16 * L.nt);
-        const int pm = G / L.pc;
-        require(G % L.pc == 0 && L.pc >= 1, "level op: bad cluster split");
-        require(c.Kp / 8 <= level_ktab_max(), "level op: k-table too long");
-        const int wrows_plan = (nchall + L.pc - 1) / L.pc * 16 * L.nt;
-        const long long wcount = (long long)L.wcount;
-        for (int m = 0; m < G; ++m) {
-            const int mp = m / L.pc, mc = m % L.pc;
-            const int ch0 = mc * nchall / L.pc, ch1 = (mc + 1) * nchall / L.pc;
-            const int p0 = mp * npt / pm * 16, p1 = std::min(P, (mp + 1) * npt / pm * 16);
-            if (p1 <= p0 || ch1 <= ch0) continue;
-            const int wrows = (ch1 - ch0) * 16 * L.nt;
-            require(wrows <= wrows_plan, "level op: weight rows exceed plan");
-            require(wrows * L.kcs * 4 <= 8 * 512, "level op: weight chunk exceeds staging registers");
-            const long long max_cout = (long long)ch1 * 16 * L.nt - 1;
-            require((max_cout + 1) * c.Kp <= wcount, "level op: weight rows outside the packed weights");
-            require(ch1 * 16 * L.nt <= L.bcount + 16, "level op: bias outside allocation");
-            for (int q0 = p0; q0 < p1; q0 += 16 * L.band) {
-                const int q1 = std::min(p1, q0 + 16 * L.band);
-                const int ho0 = q0 / c.Wo, ho1 = (q1 - 1) / c.Wo;
-                const int nrows = (ho1 - ho0) * c.stride + c.KH;
-                const long long patch_end = 16 + (long long)nrows * L.wp * L.pstride;
-                require(patch_end <= L.woff, "level op: patch overlaps the weight buffers");
-                // largest fragment read: last pixel, largest k offset
-                const int pc = q1 - 1, ho = pc / c.Wo, wo = pc - ho * c.Wo;
-                const long long lb = 16 + ((long long)(ho - ho0) * c.stride * L.wp + (long long)wo * c.stride) * L.pstride;
-                const long long kmax_off = ((long long)(c.KH - 1) * L.wp + (c.KW - 1)) * L.pstride + (c.Cin - 8) * 2;
-                require(lb + kmax_off + 16 <= patch_end, "level op: fragment read outside the patch");
-            }
-        }
-    }
-
-    void mark_syncs(int first, int last, LevelOp* lo) const {
-        struct Rng { int t, c0, c1, level; bool gpart; };
-        std::vector<Rng> w;
-        auto hit = [&](int t, int c0, int c1, bool local, int lvl) {
-            for (auto& r : w)
-                if (r.t == t && r.c0 < c1 && c0 < r.c1 && (!local || r.level != lvl || !r.gpart)) return true;
-            return false;
-        };
-        int k = 0;
-        for (int i = first; i < last; ++i) {
-            const Op& op = ops[i];
-            const int lvl = tensors[op.out.t].level;
-            if (op.kind == OP_SPPF) {
-                for (int sub = 0; sub < 3; ++sub, ++k) {
-                    const int c0 = op.out.coff + sub * op.out.C;
-                    lo[k].sync = (k == 0 || hit(op.out.t, c0, c0 + op.out.C, false, lvl)) ? 1 : 0;
-                    if (lo[k].sync) w.clear();
-                    if (k == 0) lo[k].sync = 0;
-                    w.push_back({op.out.t, c0 + op.out.C, c0 + 2 * op.out.C, lvl, true});
-                }
-                continue;
-            }
-            const bool gpart = op.kind == OP_DW || (op.kind == OP_CONV && (lo[k].kind != LOP_CONV || !lo[k].patch || lo[k].pc == 1));
-            const bool local = pixel_local(op) && gpart;
-            bool need = false;
-            for (auto& sg : op.in) need |= hit(sg.v.t, sg.v.coff, sg.v.coff + sg.v.C, local, lvl);
-            if (op.has_res) need |= hit(op.res.t, op.res.coff, op.res.coff + op.res.C, true, lvl);
-            lo[k].sync = (k > 0 && need) ? 1 : 0;
-            if (lo[k].sync) w.clear();
-            w.push_back({op.out.t, op.out.coff, op.out.coff + op.out.C, lvl, gpart});
-            ++k;
-        }
-    }
+    // ---------------------------------------------------------- launch units
+    // One launch unit per op (the unit layer stays for the profiling / segment APIs).
     void free_plans() {
-        for (auto& kv : plans)
-            if (kv.second.lops_dev) (void)hipFree(kv.second.lops_dev);
         plans.clear();
         cur_plan = nullptr;
     }
@@ -1024,78 +840,11 @@ struct Net {
         auto it = plans.find(key);
         if (it != plans.end()) { cur_plan = &it->second; return; }
         Plan pl;
-        pl.NC = std::min(32, (B + 7) / 8 * 8);
-        pl.G = 256 / pl.NC;
-        G_ = pl.G;
-        level_G_ = pl.G;
-        std::vector<LevelOp> lops;
-        size_t i = 0;
-        while (i < ops.size()) {
-            size_t j = i;
-            while (j < ops.size() && level_eligible(ops[j])) ++j;
-            bool fuse = j - i >= 2 && segment_safe((int)i, (int)j);
-            if (fuse) {   // every tensor the run touches must be addressable by a 31-bit offset
-                for (size_t k = i; k < j && fuse; ++k) {
-                    std::vector<int> ts{ops[k].out.t};
-                    for (auto& sg : ops[k].in) ts.push_back(sg.v.t);
-                    if (ops[k].has_res) ts.push_back(ops[k].res.t);
-                    for (int t : ts)
-                        if (tensor_end(t) >= ((size_t)1 << 31) - 4096) fuse = false;
-                }
-            }
-            if (fuse) {
-                Unit u{(int)i, (int)j, true, (int)lops.size(), 0};
-                for (size_t k = i; k < j; ++k) {
-                    const int subs = ops[k].kind == OP_SPPF ? 3 : 1;
-                    for (int sub = 0; sub < subs; ++sub) lops.push_back(level_op(ops[k], B, H, W, sub));
-                }
-                u.lop_cnt = (int)lops.size() - u.lop_off;
-                mark_syncs((int)i, (int)j, lops.data() + u.lop_off);
-                for (int k = u.lop_off; k < (int)lops.size(); ++k) validate_level_op(lops[k], pl.G);
-                static const bool dump = getenv("YH_LEVEL_DUMP") != nullptr;
-                if (dump) {
-                    int k = u.lop_off;
-                    for (size_t o = i; o < j; ++o) {
-                        const int subs = ops[o].kind == OP_SPPF ? 3 : 1;
-                        for (int sub = 0; sub < subs; ++sub, ++k) {
-                            const LevelOp& L = lops[k];
-                            fprintf(stderr, "[yh level] G=%d %-36s kind %d sync %d patch %d nt %d pc %d wn %d kcs %d band %d woff %d wpitch %d Cin %d Cout %d K %d Kp %d Ho %d Wo %d s %d\n",
-                                    pl.G, ops[o].label.c_str(), L.kind, L.sync, L.patch, L.nt, L.pc, L.wn, L.kcs, L.band, L.woff,
-                                    L.wpitch, L.c.Cin, L.c.Cout, L.c.K, L.c.Kp, L.c.Ho, L.c.Wo, L.c.stride);
-                        }
-                    }
-                }
-                int lds = 0;
-                for (int k = u.lop_off; k < (int)lops.size(); ++k)
-                    if (lops[k].kind == LOP_CONV && lops[k].patch) {
-                        const int nchall = (lops[k].c.Cout + 16 * lops[k].nt - 1) / (16 * lops[k].nt);
-                        const int wrows = (nchall + lops[k].pc - 1) / lops[k].pc * 16 * lops[k].nt;
-                        lds = std::max(lds, lops[k].woff + 2 * wrows * lops[k].wpitch);
-                    }
-                require(lds <= LEVEL_LDS_MAX, "level program LDS plan exceeds the budget");
-                pl.lds.push_back(lds);
-                pl.units.push_back(u);
-                i = j;
-            } else {
-                pl.units.push_back(Unit{(int)i, (int)i + 1, false, 0, 0});
-                pl.lds.push_back(0);
-                ++i;
-            }
-        }
-        if (!lops.empty()) {
-            HIPCHECK(hipMalloc(&pl.lops_dev, lops.size() * sizeof(LevelOp)));
-            HIPCHECK(hipMemcpy(pl.lops_dev, lops.data(), lops.size() * sizeof(LevelOp), hipMemcpyHostToDevice));
-            if (!bar_dev) {
-                HIPCHECK(hipMalloc(&bar_dev, (32 * 64 + 32 * 32) * sizeof(unsigned)));
-                HIPCHECK(hipMemset(bar_dev, 0, (32 * 64 + 32 * 32) * sizeof(unsigned)));
-                HIPCHECK(hipMalloc(&lerr_dev, sizeof(int)));
-                HIPCHECK(hipMemset(lerr_dev, 0, sizeof(int)));
-            }
-        }
+        for (size_t i = 0; i < ops.size(); ++i) pl.units.push_back(Unit{(int)i, (int)i + 1, false});
         cur_plan = &plans.emplace(key, std::move(pl)).first->second;
     }
     void launch_unit(const Unit& u, int B, int H, int W, hipStream_t s) {
-        launch_unit_(u, B, H, W, s);
+        for (int k = u.first; k < u.last; ++k) launch_op(k, B, H, W, s);
         // YH_SYNC_UNITS=1 (debugging): synchronize after every launch unit outside graph
         // capture, so a device fault is reported with the unit that caused it
         static const bool sync_units = getenv("YH_SYNC_UNITS") != nullptr;
@@ -1104,49 +853,12 @@ struct Net {
             (void)hipStreamIsCapturing(s, &st);
             if (st == hipStreamCaptureStatusNone) {
                 const hipError_t e = hipStreamSynchronize(s);
-                if (e != hipSuccess)
-                    throw Fail(YH_EHIP, "unit " + ops[u.first].label + (u.level ? " (level program)" : "") + ": " +
-                                            hipGetErrorString(e));
+                if (e != hipSuccess) throw Fail(YH_EHIP, "unit " + ops[u.first].label + ": " + hipGetErrorString(e));
             }
         }
     }
-    void launch_unit_(const Unit& u, int B, int H, int W, hipStream_t s) {
-        if (!u.level) { launch_op(u.first, B, H, W, s); return; }
-        static const bool dry = getenv("YH_LEVEL_DRYRUN") != nullptr;   // debugging: plan, never launch
-        if (dry) return;
-        LevelArgs a{};
-        a.ops = cur_plan->lops_dev + u.lop_off;
-        a.nops = u.lop_cnt;
-        a.B = B; a.G = cur_plan->G; a.NC = cur_plan->NC;
-        a.base = ws.base;
-        a.bar = bar_dev;
-        a.err = lerr_dev;
-        a.lds_patch = cur_plan->lds[&u - cur_plan->units.data()];
-        static const int skip = [] { const char* e = getenv("YH_LEVEL_SKIP"); return e ? atoi(e) : 0; }();
-        a.skip = skip;
-        a.trace = level_trace_ptr ? level_trace_ptr + 8 * u.lop_off : nullptr;
-        static const int plain_ok = [] { const char* e = getenv("YH_LEVEL_PLAIN"); return e ? atoi(e) : 1; }();
-        a.plain_ok = plain_ok;
-        const int rc = launch_level(dtype, a, s);
-        if (rc != 0) throw Fail(YH_EHIP, "level program launch (" + ops[u.first].label + " .. " + ops[u.last - 1].label +
-                                         ") failed: " + hipGetErrorString((hipError_t)rc));
-    }
 
-    // ---------------------------------------------------------- parallel capture
-    // The forward is a DAG (C3k's two 1x1 branches, the head's box / cls chains,
-    // the 80x80 head beside the FPN's bottom-up path, ...). When the forward is
-    // captured as a HIP graph, launch units are spread over up to par_streams
-    // streams joined by events, so the graph gets the DAG's edges and independent
-    // small kernels run side by side instead of back to back.
-    // YH_STREAMS=N (opt-in; default 1 = one serial chain). Worth ~8 % at v11_n b32 bf16
-    // (1.65 vs 1.79 ms per step), but hipGraphLaunch of these multi-branch graphs still
-    // segfaults intermittently inside libamdhip64 (ROCm 7.2) when graphs are re-captured
-    // (tests/test_gpu_conv_kernels.py), even with the mitigations kept here: graph execs
-    // destroyed only on an idle device, fork/join events kept alive with their exec, and
-    // every kernel's first launch made before capture.
-    int par_streams = [] { const char* e = getenv("YH_STREAMS"); return e ? std::max(1, std::min(8, atoi(e))) : 1; }();
-    std::vector<hipStream_t> aux_streams;
-    std::vector<hipEvent_t> unit_events;
+    // ---------------------------------------------------------- unit dependencies
     struct Rg { int t, c0, c1; };
     void unit_regions(const Unit& u, std::vector<Rg>& rd, std::vector<Rg>& wr) const {
         for (int k = u.first; k < u.last; ++k) {
@@ -1163,95 +875,6 @@ struct Net {
                 wr.push_back({op.out.t, op.out.coff, op.out.coff + op.out.C});
             }
             if (op.kind == OP_FIRST) rd.push_back({-1, 0, 1});   // the caller's x
-        }
-    }
-    void release_unit_events() {
-        for (auto e : unit_events) (void)hipEventDestroy(e);
-        unit_events.clear();
-    }
-    void run_units_parallel(int B, int H, int W, hipStream_t origin) {
-        const auto& us = cur_plan->units;
-        const int n = (int)us.size();
-        const int NS = par_streams;
-        while ((int)aux_streams.size() < NS - 1) {
-            hipStream_t st;
-            HIPCHECK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
-            aux_streams.push_back(st);
-        }
-        // fresh events per capture, never reused: forward() hands them to the graph
-        // exec they were captured into, and drop_graphs destroys them with it.
-        release_unit_events();
-        for (int i = 0; i < n + NS; ++i) {
-            hipEvent_t e;
-            HIPCHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-            unit_events.push_back(e);
-        }
-        // dependencies (RAW / WAR / WAW on channel ranges)
-        std::vector<std::vector<Rg>> rd(n), wr(n);
-        for (int i = 0; i < n; ++i) unit_regions(us[i], rd[i], wr[i]);
-        auto ov = [](const std::vector<Rg>& a, const std::vector<Rg>& b) {
-            for (auto& x : a)
-                for (auto& y : b)
-                    if (x.t == y.t && x.c0 < y.c1 && y.c0 < x.c1) return true;
-            return false;
-        };
-        std::vector<std::vector<int>> preds(n);
-        std::vector<std::vector<char>> anc(n, std::vector<char>(n, 0));   // anc[j][i]: i is an ancestor of j
-        for (int j = 0; j < n; ++j)
-            for (int i = 0; i < j; ++i)
-                if (ov(wr[i], rd[j]) || ov(rd[i], wr[j]) || ov(wr[i], wr[j])) {
-                    preds[j].push_back(i);
-                    anc[j][i] = 1;
-                    for (int k = 0; k < i; ++k) anc[j][k] |= anc[i][k];
-                }
-        // fork: every stream starts after the origin's prior work
-        std::vector<hipStream_t> st(NS);
-        st[0] = origin;
-        for (int k = 1; k < NS; ++k) st[k] = aux_streams[k - 1];
-        hipEvent_t fork = unit_events[n];
-        HIPCHECK(hipEventRecord(fork, origin));
-        for (int k = 1; k < NS; ++k) HIPCHECK(hipStreamWaitEvent(st[k], fork, 0));
-        std::vector<int> last(NS, -1);
-        std::vector<int> where(n, 0);
-        for (int j = 0; j < n; ++j) {
-            // a stream whose last unit is an ancestor adds no false dependency; prefer
-            // continuing a direct predecessor's chain, then an idle stream
-            int pick = -1, score = -1;
-            for (int k = 0; k < NS; ++k) {
-                int sc;
-                if (last[k] < 0) sc = 1;
-                else if (anc[j][last[k]]) sc = std::find(preds[j].begin(), preds[j].end(), last[k]) != preds[j].end() ? 3 : 2;
-                else sc = 0;
-                if (sc > score) { score = sc; pick = k; }
-            }
-            if (score == 0) {   // every stream is busy with concurrent work: join the oldest
-                pick = 0;
-                for (int k = 1; k < NS; ++k)
-                    if (last[k] < last[pick]) pick = k;
-            }
-            // wait for predecessors on other streams not already implied by stream order
-            std::vector<int> latest(NS, -1);
-            for (int i : preds[j]) {
-                const int si = where[i];
-                if (si == pick) continue;
-                if (last[pick] >= 0 && (last[pick] == i || anc[last[pick]][i])) continue;
-                latest[si] = std::max(latest[si], i);
-            }
-            for (int k = 0; k < NS; ++k)
-                if (latest[k] >= 0) HIPCHECK(hipStreamWaitEvent(st[pick], unit_events[latest[k]], 0));
-            launch_unit(us[j], B, H, W, st[pick]);
-            HIPCHECK(hipEventRecord(unit_events[j], st[pick]));
-            where[j] = pick;
-            last[pick] = j;
-        }
-        // join every stream back into the origin
-        for (int k = 1; k < NS; ++k) {
-            if (last[k] < 0) {   // unused stream: still has to rejoin the capture
-                HIPCHECK(hipEventRecord(unit_events[n + k], st[k]));
-            } else {
-                HIPCHECK(hipEventRecord(unit_events[n + k], st[k]));
-            }
-            HIPCHECK(hipStreamWaitEvent(origin, unit_events[n + k], 0));
         }
     }
 
@@ -1288,7 +911,6 @@ struct Net {
             auto pre = [&](const char* x) { return lb.rfind(x, 0) == 0; };
             const bool h0 = pre("head.box.0.") || pre("head.cls.0."), h1 = pre("head.box.1.") || pre("head.cls.1.");
             const bool dec = ops[u.first].kind == OP_DECODE;
-            if (u.level && (h0 || h1 || dec)) return {};   // a fused level unit spans segments
             for (int k = u.first; k < u.last; ++k) {
                 if (ops[k].label.rfind("fpn.h2", 0) == 0) last_h2 = j;
                 if (ops[k].label.rfind("fpn.h4", 0) == 0) last_h4 = j;
@@ -1419,7 +1041,7 @@ struct Net {
             run_ops(B, H, W, s);
             return;
         }
-        if (head_split && par_streams == 1 && forward_head_split(B, H, W, s)) return;
+        if (head_split && forward_head_split(B, H, W, s)) return;
         const GraphKey key{B, H, W, in_u8};
         auto it = graphs.find(key);
         if (it == graphs.end()) {
@@ -1430,15 +1052,13 @@ struct Net {
             hipGraph_t g = nullptr;
             HIPCHECK(hipStreamBeginCapture(cap_stream, hipStreamCaptureModeThreadLocal));
             try {
-                if (par_streams > 1) run_units_parallel(B, H, W, cap_stream);
-                else run_ops(B, H, W, cap_stream);
+                run_ops(B, H, W, cap_stream);
             } catch (...) {
                 (void)hipStreamEndCapture(cap_stream, &g);
-                release_unit_events();
                 if (g) (void)hipGraphDestroy(g);
                 throw;
             }
-            if (bt) fprintf(stderr, "[yh] captured B=%d H=%d W=%d streams=%d\n", B, H, W, par_streams);
+            if (bt) fprintf(stderr, "[yh] captured B=%d H=%d W=%d\n", B, H, W);
             HIPCHECK(hipStreamEndCapture(cap_stream, &g));
             if (bt) fprintf(stderr, "[yh] capture ended\n");
             hipGraphExec_t ex = nullptr;
@@ -1446,10 +1066,6 @@ struct Net {
             if (bt) fprintf(stderr, "[yh] instantiated\n");
             (void)hipGraphDestroy(g);
             it = graphs.emplace(key, ex).first;
-            // the capture's fork/join events stay alive with the exec (destroying them
-            // right after capture left a later hipGraphLaunch to segfault intermittently)
-            graph_events[key] = std::move(unit_events);
-            unit_events.clear();
         }
         HIPCHECK(hipGraphLaunch(it->second, s));
     }
@@ -1527,18 +1143,14 @@ struct Net {
     ~Net() {
         drop_graphs();
         free_plans();
-        if (bar_dev) (void)hipFree(bar_dev);
-        if (lerr_dev) (void)hipFree(lerr_dev);
         for (auto& d : convs) free_conv(d);
         if (ws.base) (void)hipFree(ws.base);
         if (io_dev) (void)hipFree(io_dev);
         if (zero_dev) (void)hipFree(zero_dev);
         if (cap_stream) (void)hipStreamDestroy(cap_stream);
-        for (auto st : aux_streams) (void)hipStreamDestroy(st);
         if (hs_stream) (void)hipStreamDestroy(hs_stream);
         for (auto e : hs_ev)
             if (e) (void)hipEventDestroy(e);
-        release_unit_events();
         for (auto e : ev) (void)hipEventDestroy(e);
     }
 };
@@ -1687,18 +1299,6 @@ size_t yh_nms_workspace_bytes(int batch, int num_classes, int anchors) {
     return (size_t)batch * anchors * num_classes * 8 + (size_t)batch * 4 + (size_t)batch * 2048 * 4 + 512;
 }
 
-// Debug hook (not part of the ABI header): yh_debug_level_trace(buf) makes later
-// level-program launches record, for block 0, s_memrealtime (100 MHz) on arrival
-// at and departure from the barrier after every level op: buf[2*k], buf[2*k+1]
-// for level op k of the plan (ops of all level units, in order); nullptr = off.
-// Graphs captured before the call keep their old setting.
-extern "C" int yh_debug_level_op_label(const yh_handle* h, int batch, int height, int width, int k,
-                                       const char** label);
-extern "C" int yh_debug_level_trace(void* device_buf) {
-    level_trace_ptr = (unsigned long long*)device_buf;
-    return 0;
-}
-
 // Debug hook (not part of the ABI header): yh_debug_nms_trace(buf) makes later
 // yh_nms calls record per-image phase timestamps into the device buffer buf
 // ([batch][16] u64, s_memrealtime ticks at 100 MHz); nullptr turns it off.
@@ -1784,24 +1384,6 @@ int yh_unit_info(const yh_handle* h, int index, int batch, int height, int width
     });
 }
 
-int yh_set_level_fusion(yh_handle* h, int enable) {
-    return guarded([&] {
-        yh::require(h, "null handle");
-        h->net.use_level = enable != 0;
-        h->net.drop_graphs();
-        h->net.conv_kern.clear();
-        h->net.cur_kern = nullptr;
-    });
-}
-
-int yh_level_status(const yh_handle* h) {
-    if (!h) return YH_EINVAL;
-    if (!h->net.lerr_dev) return 0;
-    int v = 0;
-    if (hipMemcpy(&v, h->net.lerr_dev, sizeof(int), hipMemcpyDeviceToHost) != hipSuccess) return YH_EHIP;
-    return v;
-}
-
 int yh_set_graph(yh_handle* h, int enable) {
     return guarded([&] {
         yh::require(h, "null handle");
@@ -1827,7 +1409,7 @@ int yh_profile_reset(yh_handle* h) {
 int yh_force_conv_kernel(yh_handle* h, int kernel) {
     return guarded([&] {
         yh::require(h, "null handle");
-        yh::require(kernel >= -1 && kernel < yh::CONV_NKERNELS, "conv kernel id out of range");
+        yh::require(kernel >= -1, "conv plan index out of range");
         h->net.force_kern = kernel;
         h->net.conv_kern.clear();
         h->net.cur_kern = nullptr;
@@ -1841,7 +1423,6 @@ int yh_op_kernel(const yh_handle* h, int index, int batch, int height, int width
     return guarded([&] {
         yh::require(h && index >= 0 && index < (int)h->net.ops.size(), "op index out of range");
         const yh::Net& n = h->net;
-        static const char* conv_names[] = {"gemm", "gemm64", "gemm128", "stream", "direct", "stream4", "stream8", "tiny"};
         static const char* op_names[] = {"stem", "conv", "dwconv", "sppf", "attention", "decode"};
         const yh::Op& op = n.ops[index];
         if (op.kind != yh::OP_CONV) {
@@ -1854,14 +1435,7 @@ int yh_op_kernel(const yh_handle* h, int index, int batch, int height, int width
         }
         auto it = n.conv_kern.find(yh::GraphKey{batch, height, width});
         yh::require(it != n.conv_kern.end(), "no forward has run at this shape yet", YH_ESTATE);
-        yh::ConvArgs a{};
-        int BM = 0, BN = 0;
-        n.conv_args(op, batch, height, width, a, BM, BN);
-        if (a.ks > 1) {
-            if (name) *name = a.ks == 4 ? "ksplit4" : "ksplit2";
-            return;
-        }
-        if (name) *name = conv_names[it->second[index]];
+        if (name) *name = it->second[index].name.c_str();
     });
 }
 
@@ -1889,25 +1463,6 @@ int yh_op_info(const yh_handle* h, int index, int batch, int height, int width, 
         }
         if (ms_total) *ms_total = ms;
         if (calls) *calls = nc;
-    });
-}
-
-// Label of level op k of the plan at a shape (the op it belongs to; SPPF gives 3).
-int yh_debug_level_op_label(const yh_handle* h, int batch, int height, int width, int k, const char** label) {
-    return guarded([&] {
-        yh::require(h && label, "null argument");
-        auto it = h->net.plans.find(yh::GraphKey{batch, height, width});
-        yh::require(it != h->net.plans.end(), "no plan at this shape", YH_ESTATE);
-        for (auto& u : it->second.units) {
-            if (!u.level) continue;
-            int idx = u.lop_off;
-            for (int o = u.first; o < u.last; ++o) {
-                const int subs = h->net.ops[o].kind == yh::OP_SPPF ? 3 : 1;
-                for (int sub = 0; sub < subs; ++sub, ++idx)
-                    if (idx == k) { *label = h->net.ops[o].label.c_str(); return; }
-            }
-        }
-        yh::require(false, "level op index out of range");
     });
 }
 

@@ -16,9 +16,13 @@ threshold (compared in the tensor dtype), score-descending order with ties
 broken by the lower anchor*nc + class index (the reference's argsort is
 unstable, util.py:157), first 30000 kept, class-offset boxes (class * 7680),
 greedy IoU > threshold suppression (torchvision.ops.nms contract), first 300
-kept. Deliberate differences: no wall-clock cutoff (util.py:133-134,166-167
-silently truncates batches); box geometry is evaluated in fp32 for fp16/bf16
-inputs (in fp16 the reference's class offset 7680*c overflows for c >= 9).
+kept. As in the reference, the rows come back as float32 (util.py:148: torch.cat
+with `j.float()` promotes box and score to float32, so the class offset and the
+IoU run in float32 too; the wh2xy corners are rounded to the input dtype first).
+Head outputs on a cuda device run on the MI355X kernels (yh_nms); on the CPU
+device (main.py:20 falls back to "cpu") the library's C++ host implementation
+(yh_nms_host) runs the same contract. Deliberate difference: no wall-clock
+cutoff (util.py:133-134,166-167 silently truncates batches).
 """
 import random
 
@@ -70,15 +74,13 @@ def make_anchors(x, strides, offset=0.5):
 
 
 def non_max_suppression(outputs, confidence_threshold=0.001, iou_threshold=0.65):
-    """(B, 4 + nc, A) head outputs -> list of B tensors (k <= 300, 6) = x1, y1, x2, y2, score, class."""
-    if not outputs.is_cuda:
-        raise NotImplementedError("utils.util.non_max_suppression runs on the MI355X (cuda/HIP) device; "
-                                  "move the head outputs to cuda first")
-    from yolo_hip.engine import nms
+    """(B, 4 + nc, A) head outputs -> list of B float32 tensors (k <= 300, 6) = x1, y1, x2, y2, score, class."""
+    from yolo_hip.engine import nms, nms_host
 
-    dets, counts = nms(outputs, confidence_threshold, iou_threshold, MAX_DET, MAX_NMS, float(MAX_WH))
+    run = nms if outputs.is_cuda else nms_host
+    dets, counts = run(outputs, confidence_threshold, iou_threshold, MAX_DET, MAX_NMS, float(MAX_WH))
     kept = counts.tolist()
-    return [dets[i, :k].to(outputs.dtype) for i, k in enumerate(kept)]
+    return [dets[i, :k] for i, k in enumerate(kept)]
 
 
 def load_weight(model, ckpt, trusted=False):

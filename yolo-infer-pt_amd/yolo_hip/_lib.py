@@ -13,7 +13,7 @@ from ctypes import POINTER, byref, c_char_p, c_double, c_float, c_int, c_size_t,
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libyolo_hip.so")
 
 YH_F32, YH_F16, YH_BF16 = 0, 1, 2
-ABI_VERSION = 1
+ABI_VERSION = 2
 
 
 class YhVariant(ctypes.Structure):
@@ -55,8 +55,8 @@ _PROTOS = {
     "yh_unit_count": (c_int, [c_void_p, c_int, c_int, c_int]),
     "yh_unit_info": (c_int, [c_void_p, c_int, c_int, c_int, c_int, POINTER(c_int), POINTER(c_int), POINTER(c_int),
                              POINTER(c_double), POINTER(c_int)]),
-    "yh_set_level_fusion": (c_int, [c_void_p, c_int]),
-    "yh_level_status": (c_int, [c_void_p]),
+    "yh_nms_host": (c_int, [c_int, c_void_p, c_int, c_int, c_int, c_float, c_double, c_int, c_int, c_float,
+                            c_void_p, c_void_p, c_int]),
 }
 
 _lib = None

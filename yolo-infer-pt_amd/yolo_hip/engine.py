@@ -151,18 +151,9 @@ class Engine:
         check(lib().yh_set_graph(self._h, int(bool(enable))))
 
     def force_conv_kernel(self, kernel):
-        """Run dense convs on one kernel implementation (0..7), or -1 for per-shape autotuning."""
+        """Run every 16-bit dense conv on candidate plan `kernel` of its layer (clamped to the
+        layer's last candidate), or -1 for per-shape autotuning. All plans are bit-identical."""
         check(lib().yh_force_conv_kernel(self._h, int(kernel)), "force_conv_kernel")
-
-    def set_level_fusion(self, enable):
-        """Fuse the 40x40 / 20x20 levels into level-program launches (default on, 16-bit only)."""
-        check(lib().yh_set_level_fusion(self._h, int(bool(enable))), "set_level_fusion")
-
-    def level_status(self):
-        """Raise if a level-program cluster barrier timed out (synchronizes the device)."""
-        rc = lib().yh_level_status(self._h)
-        if rc != 0:
-            raise RuntimeError(f"yolo_hip: level program barrier timeout / error ({rc})")
 
     def units(self, batch, height, width):
         """Launch units of the forward at this shape (after a forward), with profiled time."""
@@ -176,9 +167,8 @@ class Engine:
             check(lib().yh_unit_info(self._h, i, int(batch), int(height), int(width), byref(f), byref(k), byref(lv),
                                      byref(ms), byref(calls)))
             mem = ops[f.value:f.value + k.value]
-            out.append(dict(first=f.value, num_ops=k.value, level=bool(lv.value), ms=ms.value, calls=calls.value,
-                            label=mem[0]["label"] if k.value == 1 else f"level[{mem[0]['label']} .. {mem[-1]['label']}]",
-                            cls="level" if lv.value else mem[0]["cls"], kernel="level" if lv.value else mem[0]["kernel"],
+            out.append(dict(first=f.value, num_ops=k.value, ms=ms.value, calls=calls.value, label=mem[0]["label"],
+                            cls=mem[0]["cls"], kernel=mem[0]["kernel"],
                             bytes=sum(o["bytes"] for o in mem), flops=sum(o["flops"] for o in mem), ops=mem))
         return out
 
@@ -207,6 +197,24 @@ class Engine:
 class _BN:
     def __init__(self, weight, bias, mean, var, eps):
         self.weight, self.bias, self.running_mean, self.running_var, self.eps = weight, bias, mean, var, eps
+
+
+def nms_host(outputs, confidence_threshold=0.001, iou_threshold=0.65, max_det=300, max_nms=30000, max_wh=7680.0,
+             threads=0):
+    """Host (CPU) batched NMS (yh_nms_host, C++): same contract as `nms` for a CPU tensor.
+
+    Returns (dets (B, max_det, 6) f32, counts (B,) i32) CPU tensors."""
+    if outputs.is_cuda:
+        raise ValueError("yolo_hip.nms_host needs a CPU tensor")
+    y = outputs.detach().contiguous()
+    B, no, A = y.shape
+    nc = no - 4
+    dets = torch.zeros((B, max_det, 6), dtype=torch.float32)
+    counts = torch.zeros((B,), dtype=torch.int32)
+    check(lib().yh_nms_host(dtype_code(y.dtype), c_void_p(y.data_ptr()), B, nc, A, ctypes.c_float(confidence_threshold),
+                            c_double(iou_threshold), int(max_det), int(max_nms), ctypes.c_float(max_wh),
+                            c_void_p(dets.data_ptr()), c_void_p(counts.data_ptr()), int(threads)), "nms_host")
+    return dets, counts
 
 
 def nms(outputs, confidence_threshold=0.001, iou_threshold=0.65, max_det=300, max_nms=30000, max_wh=7680.0):
