@@ -498,8 +498,10 @@ __global__ __launch_bounds__(64 * NW, 2) void conv_mxr(const MxArgs p) {
 
     // ---- workgroup -> (cout slice, run of wave tiles); consecutive workgroups of an XCD adjacent
     const int L = xcd_remap(blockIdx.x, gridDim.x);
+    // slice fastest: the nslices workgroups that read the same patches run side by side
+    // on one XCD, so all but the first read of a patch hit that XCD's L2
     const int wps = gridDim.x / p.nslices;       // workgroups per slice (grid = nslices * wps)
-    const int sl = L / wps, lw = L - sl * wps;
+    const int lw = L / p.nslices, sl = L - lw * p.nslices;
     const int ntile = p.ntasks;                  // wave tiles per slice
     const int gw = lw * NW + wv, GW = wps * NW;
     const int t_lo = (int)((long long)ntile * gw / GW), t_hi = (int)((long long)ntile * (gw + 1) / GW);
@@ -986,17 +988,20 @@ std::vector<MxPlan> mx_candidates(const MxShape& sh, int num_cus) {
         }
     }
     // resident-weight per-wave kernels (instantiated set, see launch_mxr_cfg)
-    auto addr = [&](int na, int mb, int ncb, int nbi) {
+    auto addr = [&](int na, int mb, int ncb, int nbi, int nbuf = 2) {
         MxConfig c{};
         c.kind = 1; c.ks = sh.ks; c.s = sh.ks == 1 ? 1 : sh.s; c.na = na; c.mb = mb; c.wn = 1; c.wm = 8;
-        c.ncb = ncb; c.nbi = nbi; c.nbuf = (sh.ks == 3 && sh.s == 2) ? 1 : 2;
+        c.ncb = ncb; c.nbi = nbi; c.nbuf = nbuf;
         cfgs.push_back(c);
     };
     if (sh.ks == 3 && sh.s == 1) {
         if (narrow) { addr(1, 2, 1, 4); addr(1, 2, 2, 7); addr(1, 4, 1, 6); }
         else { addr(2, 2, 1, 4); addr(2, 2, 2, 7); }
     } else if (sh.ks == 3) {
-        if (narrow) addr(1, 2, 1, 10); else addr(2, 2, 1, 10);
+        // stride 2: a 4x8 wave tile (9x17 patch) double-buffered, or an 8x8 tile (17x17)
+        // single-buffered; 32-cout slices for weights too large to keep whole
+        if (narrow) { addr(1, 1, 1, 5); addr(1, 2, 1, 10, 1); }
+        else { addr(2, 1, 1, 5); addr(2, 2, 1, 10, 1); addr(1, 1, 1, 5); addr(1, 2, 1, 10, 1); }
     } else {
         if (narrow) { addr(1, 2, 1, 2); addr(1, 2, 2, 4); addr(1, 2, 4, 8); addr(1, 4, 1, 4); addr(1, 4, 2, 8); }
         else { addr(2, 2, 1, 2); addr(2, 2, 2, 4); addr(2, 2, 4, 8); }
@@ -1168,6 +1173,8 @@ int launch_mxr_cfg(const MxPlan& pl, const MxArgs& a, hipStream_t s) {
     YH_MXR(3, 1, 1, 4, 1, 6, 2)
     YH_MXR(3, 2, 2, 2, 1, 10, 1)
     YH_MXR(3, 2, 1, 2, 1, 10, 1)
+    YH_MXR(3, 2, 2, 1, 1, 5, 2)
+    YH_MXR(3, 2, 1, 1, 1, 5, 2)
     YH_MXR(1, 1, 2, 2, 1, 2, 2)
     YH_MXR(1, 1, 2, 2, 2, 4, 2)
     YH_MXR(1, 1, 2, 2, 4, 8, 2)

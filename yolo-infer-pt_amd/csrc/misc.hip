@@ -493,9 +493,132 @@ __global__ __launch_bounds__(256) void head_decode(const DecodeArgs p) {
     }
 }
 
+// 16-bit decode with the head tile staged through LDS. The head tensor's pixels are
+// ldc channels apart (box 64 | cls nc | padding), so per-anchor 16-B chunk loads
+// touch a new 128-B line per lane and every load instruction gathers 64 lines;
+// here the workgroup first copies its 256 anchors' box+cls chunks (CH per anchor)
+// as lane-consecutive 16-B pieces (each wave instruction reads whole lines), then
+// each thread decodes its anchor from LDS into registers, and the (4 + nc) x 256
+// output tile, written over the input tile, leaves as 512-B row runs.
+constexpr int DEC_A = 256;
+template <typename T, int NCC>   // NCC = nc / 8 class chunks
+__global__ __launch_bounds__(256, 2) void head_decode_lds(const DecodeArgs p) {
+    extern __shared__ __attribute__((aligned(16))) uint4 dsm4[];
+    constexpr int CH = 8 + NCC, CHP = CH + 1;   // chunks per anchor, padded LDS row
+    const int n = blockIdx.y, a0 = blockIdx.x * DEC_A;
+    const int tid = threadIdx.x;
+    const int l0 = p.H[0] * p.W[0], l1 = p.H[1] * p.W[1];
+    auto src_of = [&](int a) {   // first chunk of anchor a of image n
+        int l = 0, loc = a;
+        if (loc >= l0) { loc -= l0; l = 1; if (loc >= l1) { loc -= l1; l = 2; } }
+        return reinterpret_cast<const uint4*>(reinterpret_cast<const T*>(p.lvl[l]) +
+                                              ((long long)n * p.H[l] * p.W[l] + loc) * p.ldc);
+    };
+    {
+        constexpr int BATCH = 6;
+        const int total = DEC_A * CH;
+        for (int q0 = 0; q0 < total; q0 += 256 * BATCH) {
+            uint4 r[BATCH];
+            int dst[BATCH];
+#pragma unroll
+            for (int u = 0; u < BATCH; ++u) {
+                const int q = q0 + u * 256 + tid;
+                const int ai = q / CH, c = q - ai * CH;
+                const int a = min(a0 + ai, p.A - 1);
+                dst[u] = q < total ? ai * CHP + c : -1;
+                r[u] = q < total ? src_of(a)[c] : make_uint4(0, 0, 0, 0);
+            }
+#pragma unroll
+            for (int u = 0; u < BATCH; ++u)
+                if (dst[u] >= 0) dsm4[dst[u]] = r[u];
+        }
+    }
+    __syncthreads();
+    const int a = a0 + tid;
+    const int aa = min(a, p.A - 1);
+    int l = 0, loc = aa;
+    if (loc >= l0) { loc -= l0; l = 1; if (loc >= l1) { loc -= l1; l = 2; } }
+    const int W = p.W[l];
+    const int gy = loc / W, gx = loc - gy * W;
+    const uint4* row = dsm4 + tid * CHP;
+    float dist[4];
+#pragma unroll
+    for (int sd = 0; sd < 4; ++sd) {
+        float v[16];
+#pragma unroll
+        for (int c = 0; c < 2; ++c) {
+            Chunk<T> ch;
+            ch.v[0] = row[sd * 2 + c];
+            float f[8];
+            chunk_to_f(ch, f);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) v[c * 8 + e] = f[e];
+        }
+        float mx = v[0];
+#pragma unroll
+        for (int i = 1; i < 16; ++i) mx = fmaxf(mx, v[i]);
+        float sum = 0.f;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) { v[i] = ex<T>(v[i] - mx); sum += v[i]; }
+        float d = 0.f;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) d = fmaf((float)i, dv<T>(v[i], sum), d);
+        dist[sd] = d;
+    }
+    uint4 cls[NCC];
+#pragma unroll
+    for (int c = 0; c < NCC; ++c) cls[c] = row[8 + c];
+    __syncthreads();           // the input tile is dead: the output tile reuses it
+    T* tile = reinterpret_cast<T*>(dsm4);   // [(4 + nc)][DEC_A]
+    const float ax = (float)gx + 0.5f, ay = (float)gy + 0.5f, st = p.stride[l];
+    const float x1 = ax - dist[0], y1 = ay - dist[1];
+    const float x2 = ax + dist[2], y2 = ay + dist[3];
+    tile[0 * DEC_A + tid] = fromf<T>((x1 + x2) / 2.0f * st);
+    tile[1 * DEC_A + tid] = fromf<T>((y1 + y2) / 2.0f * st);
+    tile[2 * DEC_A + tid] = fromf<T>((x2 - x1) * st);
+    tile[3 * DEC_A + tid] = fromf<T>((y2 - y1) * st);
+#pragma unroll
+    for (int c = 0; c < NCC; ++c) {
+        Chunk<T> ch;
+        ch.v[0] = cls[c];
+        float f[8];
+        chunk_to_f(ch, f);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) tile[(4 + 8 * c + e) * DEC_A + tid] = fromf<T>(dv<T>(1.0f, 1.0f + ex<T>(-f[e])));
+    }
+    __syncthreads();
+    T* yimg = reinterpret_cast<T*>(const_cast<void*>(p.io[1])) + (long long)n * (4 + p.nc) * p.A;
+    const int rows = 4 + p.nc;
+    for (int c = tid; c < rows * (DEC_A / 8); c += 256) {
+        const int r = c / (DEC_A / 8), k = c - r * (DEC_A / 8);
+        const int a8 = a0 + 8 * k;
+        if (a8 >= p.A) continue;
+        const T* srow = tile + r * DEC_A + 8 * k;
+        T* drow = yimg + (long long)r * p.A + a8;
+        if (a8 + 8 <= p.A) st_chunk(drow, ld_chunk(srow));
+        else for (int e = 0; a8 + e < p.A; ++e) drow[e] = srow[e];
+    }
+}
+
 template <typename T>
 int launch_decode_t(const DecodeArgs& a, hipStream_t s) {
     const dim3 g((unsigned)((a.A + 255) / 256), (unsigned)a.B);
+    if constexpr (sizeof(T) == 2) {
+        // instantiated for the 80-class heads (COCO); other class counts take head_decode
+        constexpr int NCC = 10;
+        if (a.nc == 8 * NCC && a.A % 8 == 0 && a.ldc % 8 == 0 && a.ldc >= 64 + a.nc) {
+            const int lds_in = DEC_A * (8 + NCC + 1) * 16, lds_out = (4 + a.nc) * DEC_A * 2;
+            const int lds = lds_in > lds_out ? lds_in : lds_out;
+            static bool attr_set = false;
+            if (!attr_set) {
+                (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&head_decode_lds<T, NCC>),
+                                          hipFuncAttributeMaxDynamicSharedMemorySize, 80 * 1024);
+                attr_set = true;
+            }
+            hipLaunchKernelGGL((head_decode_lds<T, NCC>), g, dim3(256), lds, s, a);
+            return (int)hipGetLastError();
+        }
+    }
     const int lds = (4 + a.nc) * 256 * (int)sizeof(T);
     if (a.A % 8 == 0 && lds <= 64 * 1024) {
         hipLaunchKernelGGL((head_decode<T, true>), g, dim3(256), lds, s, a);
