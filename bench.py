@@ -60,7 +60,7 @@ def roofline(eng, args, batch, prof_steps, x, y):
     for _ in range(prof_steps):
         eng.forward(x, out=y)
     eng.profile(False)
-    ops = eng.units(batch, args.size, args.size)   # launch units: one op, or a fused level program
+    ops = eng.units(batch, args.size, args.size)   # launch units (one op each)
     by_cls = {}
     for o in ops:
         c = by_cls.setdefault(o["cls"], dict(ms=0.0, bytes=0.0, flops=0.0, launches=0, attain_ms=0.0))
@@ -69,7 +69,7 @@ def roofline(eng, args, batch, prof_steps, x, y):
         c["bytes"] += o["bytes"]
         c["flops"] += o["flops"]
         c["launches"] += 1
-        peak_tf = MFMA_PEAK_TFLOPS[args.dtype] if o["cls"] in ("conv3x3", "conv1x1", "level") else 157.3
+        peak_tf = MFMA_PEAK_TFLOPS[args.dtype] if o["cls"] in ("conv3x3", "conv1x1") else 157.3
         c["attain_ms"] += max(o["bytes"] / (HBM_PEAK_GBS * 1e9), o["flops"] / (peak_tf * 1e12)) * 1e3
     total = sum(c["ms"] for c in by_cls.values())
     for k, c in sorted(by_cls.items(), key=lambda kv: -kv[1]["ms"]):
@@ -88,7 +88,12 @@ def roofline(eng, args, batch, prof_steps, x, y):
     return dict(bound=bound, achieved=round(achieved, 1), peak=peak, unit=unit,
                 frac=round(achieved / peak, 4), traffic=traffic, traffic_source=traffic_src,
                 algorithmic_flops_per_launch=round(dom["flops"] / dom["launches"]),
-                kernel="dense 3x3 convs: conv_direct / conv_gemm2 / conv_stream implicit-GEMM MFMA, autotuned per layer",
+                kernel=("dense 3x3 convs: conv_mx (staged weights) / conv_mxr (resident weights) implicit GEMM "
+                        "on v_mfma_f32_32x32x16, LDS-DMA patch staging, plan autotuned per layer")
+                if args.dtype != "fp32" else "dense 3x3 convs: conv_gemm (fp32 FMA implicit GEMM)",
+                timing="HIP events around each launch on the forward's stream, eager (one forward at a time); "
+                       "profiles/r02_fwd_trace_ops.txt holds the rocprofv3 per-dispatch trace of the same "
+                       "forwards replayed as graphs (tools/fwd_trace.py + tools/trace_ops.py)",
                 launches_per_step=dom["launches"],
                 avg_launch_us=round(dom["ms"] * 1e3 / dom["launches"], 2),
                 algorithmic_bytes_per_launch=round(dom["bytes"] / dom["launches"]),
@@ -117,32 +122,60 @@ def pmc_traffic(cls, args):
         return None, None
 
 
-def cpu_baseline(args, min_seconds=10.0, max_seconds=30.0):
-    """The CPU oracle (fp32 functional forward + numpy NMS) on a bounded sample of the workload."""
+def _cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    import platform
+    return platform.processor() or platform.machine()
+
+
+def cpu_baseline(args, runs=3):
+    """the build's CPU restatement (oracle/, fp32 functional forward with BN
+    folded + numpy NMS) on one batch of the bench's size, torch.inference_mode(), every host
+    core this process may use, one warm-up then the median of `runs` timed runs."""
+    import statistics
+    import numpy as np
     from oracle import nms as onms
     from oracle.forward import Oracle
-    from yolo_hip import synth
     from yolo_hip.variants import VARIANTS
 
-    threads = min(16, os.cpu_count() or 1)
+    # cores this process may use: the box's CPU share (OMP_NUM_THREADS is set to it there;
+    # os.cpu_count() reports the whole machine), else the affinity mask
+    try:
+        avail = len(os.sched_getaffinity(0))
+    except AttributeError:
+        avail = os.cpu_count() or 1
+    threads = int(os.environ.get("OMP_NUM_THREADS") or avail)
+    threads = max(1, min(threads, avail))
     torch.set_num_threads(threads)
     model = build_model(args.variant)
     v = VARIANTS[args.variant]
     orc = Oracle(model.state_dict(), v.width, v.depth, v.csp, 80, dtype=torch.float32)
-    per = 4
-    x = synth.synth_scenes(per, args.size, args.size, seed=1000)
-    orc(x[:1])  # warm-up
-    n, t0 = 0, time.perf_counter()
-    while True:
-        y = orc(x)
-        onms.non_max_suppression(y.numpy())
-        n += per
-        dt = time.perf_counter() - t0
-        if dt >= min_seconds or dt >= max_seconds:
-            break
-    return dict(value=round(n / dt, 3), unit="images/s", cores=threads, kind="port",
-                sample=f"{n} images ({n // per} batches of {per}) of the same workload "
-                       f"(v11_{args.variant} {args.size}x{args.size}, fp32 oracle forward + numpy NMS), {dt:.1f} s")
+    B = args.batch
+    g = torch.Generator().manual_seed(0)
+    x = torch.rand(B, 3, args.size, args.size, generator=g)   # BASELINE.md §3 inputs
+
+    def once():
+        t0 = time.perf_counter()
+        with torch.inference_mode():
+            y = orc(x)
+        onms.non_max_suppression(np.ascontiguousarray(y.numpy()))
+        return time.perf_counter() - t0
+
+    once()   # warm-up
+    times = [once() for _ in range(runs)]
+    med = statistics.median(times)
+    return dict(value=round(B / med, 3), unit="images/s", cores=threads, kind="port",
+                cpu_model=_cpu_model(), host_cpus_visible=os.cpu_count(),
+                runs_s=[round(t, 3) for t in times],
+                sample=f"batch {B} (torch.rand seed 0, {args.size}x{args.size}), v11_{args.variant} fp32 oracle "
+                       f"forward (BN folded) + numpy NMS; 1 warm-up + median of {runs} runs, "
+                       f"{threads} threads, torch.inference_mode()")
 
 
 def main():
@@ -170,7 +203,9 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    dist = world > 1
+    # launched by torch.distributed.run (RANK + MASTER_ADDR set): a process group even at
+    # world size 1, so the RCCL gather of the results runs on the device in every such run
+    dist = world > 1 or ("RANK" in os.environ and "MASTER_ADDR" in os.environ)
     if dist:
         torch.cuda.set_device(local)
         torch.distributed.init_process_group("nccl", device_id=torch.device("cuda", local))
@@ -197,7 +232,7 @@ def main():
     x = synth.synth_scenes(B, S, S, seed=100 + rank).to(dev, dtype)
     A = eng.num_anchors(S, S)
     y = torch.empty((B, 84, A), dtype=dtype, device=dev)
-    gather = Gather(B, 300, dev, rank, world)
+    gather = Gather(B, 300, dev, rank, world, slots=2 * args.lanes + 2)   # >= batches in flight
 
     post = (lambda d, c: gather(d, c)) if dist else None  # RCCL gather of the fixed-size results to rank 0
     engs = [eng]
@@ -215,11 +250,10 @@ def main():
         if args.serial:
             eng.forward(x, out=y)
             dets, counts = nms(y)
-            if dist:
-                post(dets, counts)
-            return counts
+            extra = post(dets, counts) if dist else None
+            return dets, counts, extra
         # forward of this batch overlaps the NMS (+ gather) of the previous one
-        return pipe.submit(x)[1]
+        return pipe.submit(x)[:3]
 
     for _ in range(args.warmup):
         step()
@@ -229,7 +263,7 @@ def main():
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        counts = step()
+        last = step()
     torch.cuda.synchronize()
     if dist:
         torch.distributed.barrier()
@@ -239,7 +273,13 @@ def main():
         t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
         elapsed = t.item()
+    dets, counts, extra = last
     kept = counts.cpu().tolist()
+    gather_check = None
+    if dist and rank == 0:
+        # the last step's gathered rows of rank 0 are its own NMS results
+        from yolo_hip.dist import pack
+        gather_check = bool(torch.equal(extra[0], pack(dets, counts)))
 
     roof = None
     if not args.no_roofline:
@@ -276,6 +316,8 @@ def main():
                 "2-stream pipeline (forward k+1 overlaps NMS k)" if args.lanes == 1 else
                 f"{args.lanes} forward lanes (forwards of consecutive batches overlap) + NMS stream"),
             "kept_last_step": kept[:4],
+            "gather": (f"RCCL gather of packed detections to rank 0 over {world} rank(s), "
+                       f"last step rank-0 rows match: {gather_check}") if dist else None,
         }
         print(json.dumps(rec), flush=True)
     if dist:

@@ -17,6 +17,9 @@
  *   yh_forward_u8       main.py:265-267     uint8 -> dtype, / 255 preprocessing fused into yh_forward's stem
  *   yh_nms              utils/util.py:123-169 non_max_suppression (+ torchvision.ops.nms, util.py:162)
  *   yh_nms_host         the same for head outputs on the CPU device (main.py:20 device fallback)
+ *   yh_letterbox        utils/dataset.py:95-103, 292-313, 86-88: eval-mode load_image resize
+ *                       (cv2 INTER_LINEAR) + zero border + HWC->CHW, BGR->RGB, on the device
+ *   yh_letterbox_host   the same on the host (Dataset.__getitem__ in the loader workers)
  *
  * Conventions
  *   - Every function returns 0 on success and a negative YH_E* code on failure;
@@ -153,6 +156,27 @@ int yh_nms(int dtype, const void* y, int batch, int num_classes, int anchors,
 int yh_nms_host(int dtype, const void* y, int batch, int num_classes, int anchors,
                 float conf_threshold, double iou_threshold, int max_det, int max_nms,
                 float max_wh, float* dets, int* counts, int threads);
+
+/* Letterbox geometry of one image for a square canvas of `size` (dataset.py:95-103,
+ * 292-313): resized height / width (int(h * r), int(w * r) with r = size / max(h, w);
+ * unchanged when r == 1) and the top / left border. */
+int yh_letterbox_geometry(int height, int width, int size, int* new_h, int* new_w, int* top, int* left);
+
+/* Eval-mode preprocessing of a batch of decoded images, on the device:
+ *   srcs[i]: device uint8 HWC BGR image of heights[i] x widths[i], row stride
+ *            strides[i] bytes (strides may be NULL: 3 * width)
+ *   dst:     device uint8 (batch, 3, size, size) RGB CHW: the image resized as
+ *            cv2.resize INTER_LINEAR does (11-bit fixed point; exact 2x
+ *            downscales as INTER_AREA) and centred on a zero border.
+ * Asynchronous on `stream`. yh_letterbox_host computes the same bytes for one
+ * image in host memory (dst (3, size, size)); `threads` > 1 splits the rows. */
+int yh_letterbox(const void* const* srcs, const int* heights, const int* widths, const int* strides,
+                 int batch, int size, void* dst, void* stream);
+int yh_letterbox_host(const void* src, int height, int width, int stride, int size, void* dst, int threads);
+
+/* cv2.resize(src, (new_w, new_h), INTER_LINEAR) of one uint8 HWC 3-channel host image
+ * (the resize step alone; dst is new_h x new_w x 3, channel order kept). */
+int yh_resize_linear_host(const void* src, int height, int width, int stride, int new_h, int new_w, void* dst);
 
 /* Per-op instrumentation (bench / roofline). With profiling enabled,
  * yh_forward launches the ops eagerly with a HIP event pair around each op on

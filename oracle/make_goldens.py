@@ -17,6 +17,9 @@ sha256 is stored):
       nets.nn.yolo_v11_n() after torch.manual_seed(0) (constructor parity).
   nms_synth.npz       reference non_max_suppression on synthetic head outputs.
   nms_forward_n640.npz  reference non_max_suppression on the v11_n 640 golden output.
+  forward_x_1280_b1_sub.npz  (--x1280) v11_x at 1280x1280 (C5's shape, PSA over 1600
+      tokens): the float64 output at 4096 seeded anchors, per-row sums, the reference
+      NMS detections and the float32 / bfloat16 / float16 deviation statistics.
 
 Usage: PYTHONDONTWRITEBYTECODE=1 python oracle/make_goldens.py
 """
@@ -114,6 +117,46 @@ def forward_golden(ref_nn, synth, variant, size, batch, seed=5):
     return y64
 
 
+def forward_golden_sub(ref_nn, ref_util, synth, variant, size, batch, seed=5, n_sub=4096):
+    """Large-shape golden kept small: the float64 reference output at n_sub seeded anchors of
+    every image (all 4 + nc rows), its per-row sums over all anchors (float64), the
+    reference NMS detections of the full float64 output, and the deviation statistics of
+    the reference's own float32 / bfloat16 / float16 CPU forwards over the full output."""
+    import copy
+    torch.manual_seed(0)
+    model = getattr(ref_nn, f"yolo_v11_{variant}")(80)
+    model.load_state_dict(synth.synth_state_dict(model.state_dict(), seed=0))
+    model.eval().fuse()
+    x = synth.synth_scenes(batch, size, size, seed=seed)
+    t0 = time.time()
+    with torch.no_grad():
+        y64d = copy.deepcopy(model).double()(x.double())
+        y64 = y64d.float().numpy()
+        y32 = model(x).numpy()
+        yb = copy.deepcopy(model).bfloat16()(x.bfloat16()).float().numpy()
+        try:
+            yh = copy.deepcopy(model).half()(x.half()).float().numpy()
+        except Exception as e:  # noqa: BLE001
+            print("  fp16 CPU forward unavailable:", e)
+            yh = None
+    A = y64.shape[2]
+    idx = np.sort(np.random.default_rng(1234).choice(A, size=min(n_sub, A), replace=False)).astype(np.int64)
+    dets = ref_util.non_max_suppression(torch.from_numpy(y64), 0.001, 0.65)
+    counts, flat = pack_dets(dets)
+    out = dict(y_sub=y64[:, :, idx], idx=idx, row_sum=y64d.sum(dim=2).numpy(), anchors=np.array(A),
+               dets=flat, counts=counts, x_sha256=np.array(synth.sha256(x)),
+               dev_fp32_8thr=stats(y32, y64), dev_bf16=stats(yb, y64))
+    if yh is not None:
+        out["dev_fp16"] = stats(yh, y64)
+    out["meta"] = np.array(json.dumps(dict(variant=variant, size=size, batch=batch, input="synth_scenes",
+                                           input_seed=seed, weight_seed=0, torch=torch.__version__,
+                                           subsample=int(len(idx)))))
+    path = os.path.join(GOLD, f"forward_{variant}_{size}_b{batch}_sub.npz")
+    np.savez_compressed(path, **out)
+    print(f"  {os.path.basename(path)}: fp32 box {out['dev_fp32_8thr'][0]:.2e}; bf16 box {out['dev_bf16'][0]:.2e} "
+          f"cls {out['dev_bf16'][2]:.2e}; kept {counts.tolist()} ({time.time() - t0:.0f}s)")
+
+
 def construct_golden(ref_nn):
     torch.manual_seed(0)
     m = ref_nn.yolo_v11_n(80)
@@ -160,6 +203,9 @@ def main():
     ref_nn, ref_util = import_reference()
     os.makedirs(GOLD, exist_ok=True)
     torch.set_num_threads(8)
+    if "--x1280" in sys.argv:   # the large C5 golden alone (minutes of CPU)
+        forward_golden_sub(ref_nn, ref_util, synth, "x", 1280, 1)
+        return
     print("constructor parity")
     construct_golden(ref_nn)
     print("forward goldens")

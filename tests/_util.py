@@ -64,3 +64,38 @@ def noise_floor(g, key):
 
 def meta(g):
     return json.loads(str(g["meta"]))
+
+
+def box_iou(a, b):
+    """IoU matrix of (n, 4) and (m, 4) x1y1x2y2 boxes (float64 numpy)."""
+    a = np.asarray(a, dtype=np.float64)[:, None, :]
+    b = np.asarray(b, dtype=np.float64)[None, :, :]
+    iw = np.clip(np.minimum(a[..., 2], b[..., 2]) - np.maximum(a[..., 0], b[..., 0]), 0, None)
+    ih = np.clip(np.minimum(a[..., 3], b[..., 3]) - np.maximum(a[..., 1], b[..., 1]), 0, None)
+    inter = iw * ih
+    area = lambda x: (x[..., 2] - x[..., 0]) * (x[..., 3] - x[..., 1])
+    return inter / np.maximum(area(a) + area(b) - inter, 1e-12)
+
+
+def detection_match(got, want, top=100, iou_min=0.5):
+    """Detection-set match of `got` against the reference detections `want` ((k, 6) rows
+    x1 y1 x2 y2 score class, score-descending): each of want's `top` highest-scoring
+    detections is matched greedily (in score order) to an unused detection of the same class
+    in got with the highest IoU. Returns (fraction matched with IoU >= iou_min, mean IoU over
+    want's top detections, unmatched counting 0)."""
+    got = np.asarray(got, dtype=np.float64)
+    want = np.asarray(want, dtype=np.float64)[:top]
+    if len(want) == 0:
+        return 1.0, 1.0
+    used = np.zeros(len(got), dtype=bool)
+    ious = np.zeros(len(want))
+    if len(got):
+        iou = box_iou(want[:, :4], got[:, :4])
+        for i in range(len(want)):
+            cand = np.where((got[:, 5] == want[i, 5]) & ~used)[0]
+            if len(cand):
+                j = cand[np.argmax(iou[i, cand])]
+                if iou[i, j] > 0:
+                    ious[i] = iou[i, j]
+                    used[j] = True
+    return float((ious >= iou_min).mean()), float(ious.mean())

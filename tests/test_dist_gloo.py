@@ -59,6 +59,24 @@ def _worker(rank, world, port, out_path):
         torch.distributed.destroy_process_group()
 
 
+def _worker_pipelined(rank, world, port, out_path):
+    """Two batches gathered back to back (as DetectPipeline queues them) before batch 0 is read."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.distributed.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        per = 2
+        g = dist.Gather(per, MAX_DET, "cpu", rank, world, slots=2)
+        got = []
+        for k in range(2):   # batch k covers global images [k*per*world, (k+1)*per*world)
+            lo = k * per * world + rank * per
+            dets, counts = _batch_detections(lo, lo + per)
+            got.append(g(dets, counts))
+        if rank == 0:
+            torch.save([[t.clone() for t in g.detections(r)] for r in got], out_path)
+    finally:
+        torch.distributed.destroy_process_group()
+
+
 def test_shard_covers_every_image_once():
     for total in (0, 1, 7, 32, 256, 257):
         for world in (1, 2, 3, 8):
@@ -87,3 +105,29 @@ def test_gather_world2_gloo(tmp_path):
     assert len(got) == TOTAL
     for i in range(TOTAL):
         assert torch.equal(got[i], want_d[i, :want_c[i]]), f"image {i}"
+
+
+def test_gather_pipelined_batches_keep_their_own_buffers(tmp_path):
+    """batch k's gathered rows must survive batch k+1's gather (buffer ring)."""
+    out = str(tmp_path / "dets2.pt")
+    mp.spawn(_worker_pipelined, args=(2, _free_port(), out), nprocs=2, join=True)
+    got = torch.load(out, weights_only=True)
+    want_d, want_c = _batch_detections(0, 8)
+    assert [len(b) for b in got] == [4, 4]
+    for k in range(2):
+        for i in range(4):
+            j = 4 * k + i
+            assert torch.equal(got[k][i], want_d[j, :want_c[j]]), f"batch {k} image {i}"
+
+
+def test_gather_without_process_group_single_rank():
+    dets, counts = _batch_detections(0, 2)
+    g = dist.Gather(2, MAX_DET, "cpu", 0, 1, slots=2)
+    a = g(dets, counts)
+    b = g(torch.zeros_like(dets), torch.zeros_like(counts))
+    assert a is not b
+    flat = g.detections(a)
+    for i in range(2):
+        assert torch.equal(flat[i], dets[i, :counts[i]])
+    with pytest.raises(RuntimeError):
+        dist.Gather(2, MAX_DET, "cpu", 0, 2)(dets, counts)

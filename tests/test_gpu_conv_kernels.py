@@ -18,7 +18,7 @@ pytestmark = pytest.mark.gpu
 
 
 @pytest.mark.parametrize("variant,dtype,batch,size", [("n", torch.bfloat16, 32, 640), ("n", torch.float16, 4, 640),
-                                                      ("s", torch.float16, 8, 640)])
+                                                      ("s", torch.float16, 64, 640), ("x", torch.bfloat16, 1, 1280)])
 def test_all_conv_plans_bit_identical(gpu, variant, dtype, batch, size):
     from nets import nn
     from yolo_hip.engine import Engine

@@ -35,3 +35,38 @@ def test_uint8_input_matches_torch_preprocessing(gpu, dtype):
     eng.set_graph(True)
     assert torch.equal(eng.forward(x8.to(dtype) / 255.), want)
     assert torch.equal(eng.forward(x8), want)
+
+
+def test_device_letterbox_matches_host_path(gpu):
+    """yh_letterbox (one kernel per 32 images) == yh_letterbox_host per image (same per-pixel
+    code), for a batch of mixed sizes larger than one launch, host and device sources."""
+    import numpy as np
+    from yolo_hip import preprocess as pre
+    rng = np.random.default_rng(3)
+    shapes = [(480, 640), (640, 427), (1280, 1280), (1280, 960), (17, 23), (640, 640), (720, 1280), (33, 1000)]
+    imgs = [rng.integers(0, 256, shapes[i % len(shapes)] + (3,), dtype=np.uint8) for i in range(37)]
+    want = np.stack([pre.letterbox_host(im, 640) for im in imgs])
+    got = pre.letterbox([torch.from_numpy(im).to(gpu) for im in imgs], 640)
+    torch.cuda.synchronize()
+    assert got.shape == (37, 3, 640, 640) and got.dtype == torch.uint8
+    assert np.array_equal(got.cpu().numpy(), want)
+    got2 = pre.letterbox(imgs[:3], 320, device=gpu)
+    assert np.array_equal(got2.cpu().numpy(), np.stack([pre.letterbox_host(im, 320) for im in imgs[:3]]))
+
+
+def test_letterboxed_batch_runs_through_forward_u8(gpu):
+    import numpy as np
+    from nets import nn
+    from yolo_hip import preprocess as pre
+    from yolo_hip.engine import Engine
+    torch.manual_seed(0)
+    model = nn.yolo_v11_n(80)
+    model.load_state_dict(synth.synth_state_dict(model.state_dict(), seed=0))
+    eng = Engine(*model._yh_arch, gpu, torch.bfloat16)
+    eng.load_module(model.eval())
+    rng = np.random.default_rng(4)
+    imgs = [rng.integers(0, 256, s + (3,), dtype=np.uint8) for s in ((480, 640), (640, 480), (300, 500))]
+    x8 = pre.letterbox([torch.from_numpy(im).to(gpu) for im in imgs], 640)
+    y = eng.forward(x8).clone()
+    ref = eng.forward(torch.from_numpy(np.stack([pre.letterbox_host(im, 640) for im in imgs])).to(gpu)).clone()
+    assert torch.equal(y, ref)

@@ -1,0 +1,157 @@
+"""Eval preprocessing of the loader (the data format before the
+path): the library's host letterbox (yh_letterbox_host, yh_resize_linear_host) against
+the numpy restatement in oracle/preprocess.py (bit-exact), that restatement against
+torch's half-pixel bilinear resize (within one grey level: cv2 itself is absent, so
+parity with cv2 is unpinned), and the drop-in utils.dataset on a small on-disk set.
+The device kernel (yh_letterbox) is pinned to the host path in test_gpu_preprocess.py.
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+from oracle import preprocess as opre
+from yolo_hip import preprocess as pre
+
+from conftest import GOLD
+
+SHAPES = [(480, 640, 640), (1000, 750, 640), (300, 200, 640), (1280, 1280, 640), (1280, 960, 640),
+          (1279, 853, 640), (17, 23, 64), (640, 640, 640), (720, 1280, 640), (33, 1000, 320), (2, 3, 64),
+          (1, 1, 32), (427, 640, 640), (640, 427, 640), (5000, 40, 640)]
+
+
+def _img(h, w, seed):
+    rng = np.random.default_rng(seed)
+    base = rng.integers(0, 256, (h, w, 3), dtype=np.uint8)
+    if h > 4 and w > 4:   # smooth gradients + noise: exercises rounding at every level
+        yy, xx = np.mgrid[0:h, 0:w]
+        base[..., 0] = ((xx * 255) // max(1, w - 1)).astype(np.uint8)
+    return base
+
+
+def test_geometry_matches_restatement():
+    for h in (1, 2, 31, 320, 427, 479, 480, 481, 639, 640, 641, 1000, 1279, 4000):
+        for w in (1, 3, 64, 333, 640, 853, 1280, 3000):
+            for s in (32, 320, 640, 1280):
+                want = opre.geometry(h, w, s)
+                if min(want[:2]) < 1:   # the reference's cv2.resize would reject a 0-pixel side
+                    with pytest.raises(RuntimeError):
+                        pre.geometry(h, w, s)
+                    continue
+                assert pre.geometry(h, w, s) == want, (h, w, s)
+
+
+@pytest.mark.parametrize("h,w,s", SHAPES)
+def test_host_letterbox_bit_exact_vs_restatement(h, w, s):
+    img = _img(h, w, h * 7 + w)
+    want = opre.letterbox(img, s)
+    assert np.array_equal(pre.letterbox_host(img, s), want)
+    assert np.array_equal(pre.letterbox_host(img, s, threads=4), want)
+    # strided source (a crop of a wider buffer)
+    wide = np.zeros((h, w + 5, 3), dtype=np.uint8)
+    wide[:, :w] = img
+    assert np.array_equal(pre.letterbox_host(wide[:, :w], s), want)
+
+
+@pytest.mark.parametrize("h,w,nh,nw", [(480, 640, 240, 320), (480, 640, 479, 641), (100, 100, 37, 211),
+                                       (7, 9, 640, 480), (640, 480, 640, 480)])
+def test_resize_linear_host_vs_restatement_and_torch(h, w, nh, nw):
+    img = _img(h, w, 3)
+    got = pre.resize_linear_host(img, nh, nw)
+    assert np.array_equal(got, opre.resize_linear(img, nh, nw))
+    if (h, w) != (2 * nh, 2 * nw):
+        t = torch.from_numpy(img).permute(2, 0, 1)[None].float()
+        ref = F.interpolate(t, size=(nh, nw), mode="bilinear", align_corners=False)[0].permute(1, 2, 0)
+        assert (torch.from_numpy(got).float() - ref).abs().max().item() <= 1.0 + 1e-3
+
+
+def test_restatement_within_one_level_of_torch_bilinear():
+    for h, w, s in SHAPES:
+        img = _img(h, w, 11)
+        nh, nw, top, left = opre.geometry(h, w, s)
+        if (h, w) == (2 * nh, 2 * nw):
+            continue
+        t = torch.from_numpy(img).permute(2, 0, 1)[None].float()
+        ref = F.interpolate(t, size=(nh, nw), mode="bilinear", align_corners=False)[0].flip(0)
+        got = torch.from_numpy(opre.letterbox(img, s)[:, top:top + nh, left:left + nw].astype(np.float32))
+        assert (got - ref).abs().max().item() <= 1.0 + 1e-3, (h, w, s)
+
+
+def test_public_api_names_cover_reference_modules():
+    """Every top-level def / class of the reference's utils/util.py, utils/dataset.py and nets/nn.py
+    exists in the drop-in (tests/golden/ref_api_names.json, made by make_ref_api_names.py);
+    the training-side ones fail loudly."""
+    from nets import nn
+    from utils import dataset, util
+    with open(os.path.join(GOLD, "ref_api_names.json")) as f:
+        names = json.load(f)
+    for mod, key in ((util, "utils/util"), (dataset, "utils/dataset"), (nn, "nets/nn")):
+        missing = [n for n in names[key] if not hasattr(mod, n)]
+        assert not missing, (key, missing)
+    for n in util.OUT_OF_SCOPE:
+        with pytest.raises(NotImplementedError):
+            getattr(util, n)()
+    for n in dataset.OUT_OF_SCOPE:
+        with pytest.raises(NotImplementedError):
+            getattr(dataset, n)()
+    m = util.AverageMeter()
+    m.update(2.0, 3)
+    m.update(float("nan"), 5)
+    m.update(4.0, 1)
+    assert m.num == 4 and m.avg == pytest.approx(2.5)
+
+
+def _write_set(root, shapes):
+    from PIL import Image
+    imgs, files = [], []
+    os.makedirs(os.path.join(root, "images", "val"), exist_ok=True)
+    os.makedirs(os.path.join(root, "labels", "val"), exist_ok=True)
+    for i, (h, w) in enumerate(shapes):
+        rgb = _img(h, w, 100 + i)[:, :, ::-1]
+        fn = os.path.join(root, "images", "val", f"{i:03d}.png")
+        Image.fromarray(np.ascontiguousarray(rgb)).save(fn)
+        with open(os.path.join(root, "labels", "val", f"{i:03d}.txt"), "w") as f:
+            if i % 3 != 2:   # every third image has no labels
+                f.write(f"{i % 80} 0.5 0.5 0.25 0.4\n3 0.2 0.3 0.1 0.1\n")
+        imgs.append(np.ascontiguousarray(rgb[:, :, ::-1]))
+        files.append(fn)
+    return files, imgs
+
+
+def test_dataset_eval_items_and_collate(tmp_path):
+    from utils import dataset
+    shapes = [(480, 640), (640, 427), (300, 300), (1280, 960), (200, 640)]
+    files, imgs = _write_set(str(tmp_path), shapes)
+    ds = dataset.Dataset(files, 640, {}, augment=False)
+    assert len(ds) == len(files)
+    items = [ds[i] for i in range(len(ds))]
+    for i, (sample, cls, box, idx) in enumerate(items):
+        assert sample.dtype == torch.uint8 and sample.shape == (3, 640, 640)
+        assert np.array_equal(sample.numpy(), opre.letterbox(imgs[i], 640))
+        # the reference's two-step route: load_image, resize (pad), CHW + BGR->RGB
+        im, (h0, w0) = ds.load_image(i)
+        padded, ratio, pad = dataset.resize(im, 640, False)
+        assert ratio == (1.0, 1.0)
+        assert np.array_equal(np.ascontiguousarray(padded.transpose(2, 0, 1)[::-1]), sample.numpy())
+        n = 0 if i % 3 == 2 else 2
+        assert cls.shape == (n, 1) and box.shape == (n, 4) and idx.shape == (n,)
+        if n:
+            nh, nw, _, _ = pre.geometry(h0, w0, 640)
+            cx = (0.5 * nw + (640 - nw) / 2) / 640
+            assert box[0, 0].item() == pytest.approx(cx, abs=1e-5)
+            assert box[0, 2].item() == pytest.approx(0.25 * nw / 640, abs=1e-5)
+    samples, targets = dataset.Dataset.collate_fn(items)
+    assert samples.shape == (5, 3, 640, 640)
+    assert targets["cls"].shape[0] == targets["box"].shape[0] == targets["idx"].shape[0] == 8
+    assert targets["idx"].tolist() == [0, 0, 1, 1, 3, 3, 4, 4]
+    raw = [ds.raw(i) for i in range(2)]
+    samples, _ = dataset.Dataset.collate_fn(raw)
+    assert isinstance(samples, list) and samples[0].shape == (480, 640, 3)
+    # the label cache (no pickle) round-trips
+    again = dataset.Dataset(files, 640, {}, augment=False)
+    assert all(np.array_equal(a, b) for a, b in zip(ds.labels, again.labels))
+    with pytest.raises(NotImplementedError):
+        dataset.Dataset(files, 640, {}, augment=True)

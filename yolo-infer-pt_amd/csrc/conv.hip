@@ -129,11 +129,11 @@ __global__ __launch_bounds__(NT_) void conv_gemm(const ConvArgs p) {
     };
     (void)rb; (void)bload;
 
-    f32x4 acc[NTL][MT];
+    typename Mma<T>::acc_t acc[NTL][MT];
 #pragma unroll
     for (int i = 0; i < NTL; ++i)
 #pragma unroll
-        for (int j = 0; j < MT; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+        for (int j = 0; j < MT; ++j) acc[i][j] = typename Mma<T>::acc_t{0, 0, 0, 0};
 
     const int nkt = p.Kp / BK;
     load_tile(0);
@@ -172,19 +172,22 @@ __global__ __launch_bounds__(NT_) void conv_gemm(const ConvArgs p) {
     T* Cs = reinterpret_cast<T*>(smem);
 #pragma unroll
     for (int i = 0; i < NTL; ++i) {
-        const int co = i * 16 + (lane >> 4) * 4;
+        int co[4];
         float bv[4];
 #pragma unroll
-        for (int r = 0; r < 4; ++r) bv[r] = p.bias[n0 + co + r];
+        for (int r = 0; r < 4; ++r) {
+            co[r] = i * 16 + Mma<T>::row(lane >> 4, r);
+            bv[r] = p.bias[n0 + co[r]];
+        }
 #pragma unroll
         for (int j = 0; j < MT; ++j) {
             const int px = wave * (BM / 4) + j * 16 + fr;
-            T* dst = Cs + px * LDE + co;
+            T* dst = Cs + px * LDE;
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
-                float v = acc[i][j][r] + bv[r];
+                float v = Mma<T>::finish(acc[i][j][r], bv[r]);
                 if (p.act == ACT_SILU) v = silu<T>(v);
-                dst[r] = fromf<T>(v);
+                dst[co[r]] = fromf<T>(v);
             }
         }
     }

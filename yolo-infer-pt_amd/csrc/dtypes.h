@@ -63,8 +63,21 @@ template <> __device__ __forceinline__ float silu<float>(float x) { return x / (
 // k values of its row (A) / column (B). For f32 the 32-deep step is eight exact
 // f32 MFMAs (16x16x4); the k permutation is the same for A and B, so the sum is
 // over the same 32 products.
+typedef double f64x4 __attribute__((ext_vector_type(4)));
+
+// One 16x16 x K=32-bytes-of-operands MFMA step of conv_gemm. acc_t is the accumulator
+// type; finish() adds the bias and rounds to float. The 16-bit paths accumulate in
+// fp32 (16x16x32); the fp32 (parity) path runs v_mfma_f64_16x16x4f64 on the fp32
+// operands widened to fp64: the products are exact and the K sums carry no fp32
+// rounding, so a layer's only fp32 rounding is its output's (a sequential fp32 chain
+// over K = 576..2304 made the fp32 forward several times noisier than the reference's
+// blocked CPU sums).
 template <typename T> struct Mma;
 template <> struct Mma<__bf16> {
+    typedef f32x4 acc_t;
+    static __device__ __forceinline__ float finish(float a, float b) { return a + b; }
+    // output row (cout within the 16-tile) of accumulator register r in lane group q = lane / 16
+    static __device__ __forceinline__ int row(int q, int r) { return 4 * q + r; }
     static __device__ __forceinline__ void step(f32x4& acc, const uint4* a, const uint4* b) {
         bf16x8 av = __builtin_bit_cast(bf16x8, a[0]);
         bf16x8 bv = __builtin_bit_cast(bf16x8, b[0]);
@@ -72,6 +85,10 @@ template <> struct Mma<__bf16> {
     }
 };
 template <> struct Mma<_Float16> {
+    typedef f32x4 acc_t;
+    static __device__ __forceinline__ float finish(float a, float b) { return a + b; }
+    // output row (cout within the 16-tile) of accumulator register r in lane group q = lane / 16
+    static __device__ __forceinline__ int row(int q, int r) { return 4 * q + r; }
     static __device__ __forceinline__ void step(f32x4& acc, const uint4* a, const uint4* b) {
         f16x8 av = __builtin_bit_cast(f16x8, a[0]);
         f16x8 bv = __builtin_bit_cast(f16x8, b[0]);
@@ -79,12 +96,16 @@ template <> struct Mma<_Float16> {
     }
 };
 template <> struct Mma<float> {
-    static __device__ __forceinline__ void step(f32x4& acc, const uint4* a, const uint4* b) {
+    typedef f64x4 acc_t;
+    static __device__ __forceinline__ float finish(double a, float b) { return (float)(a + (double)b); }
+    // v_mfma_f64_16x16x4f64 interleaves the rows: register r of lane group q holds row q + 4 r
+    static __device__ __forceinline__ int row(int q, int r) { return q + 4 * r; }
+    static __device__ __forceinline__ void step(f64x4& acc, const uint4* a, const uint4* b) {
         const float* af = reinterpret_cast<const float*>(a);
         const float* bf = reinterpret_cast<const float*>(b);
 #pragma unroll
         for (int kk = 0; kk < 8; ++kk)
-            acc = __builtin_amdgcn_mfma_f32_16x16x4f32(af[kk], bf[kk], acc, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f64_16x16x4f64((double)af[kk], (double)bf[kk], acc, 0, 0, 0);
     }
 };
 

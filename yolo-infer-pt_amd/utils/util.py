@@ -24,6 +24,8 @@ device (main.py:20 falls back to "cpu") the library's C++ host implementation
 (yh_nms_host) runs the same contract. Deliberate difference: no wall-clock
 cutoff (util.py:133-134,166-167 silently truncates batches).
 """
+import math
+import os
 import random
 
 import numpy
@@ -31,8 +33,52 @@ import torch
 
 from yolo_hip.metrics import compute_ap, compute_metric, smooth  # noqa: F401
 
-__all__ = ["setup_seed", "wh2xy", "make_anchors", "non_max_suppression", "load_weight",
-           "load_ultralytics_weight", "compute_metric", "compute_ap", "smooth"]
+__all__ = ["setup_seed", "setup_multi_processes", "wh2xy", "make_anchors", "non_max_suppression", "load_weight",
+           "load_ultralytics_weight", "compute_metric", "compute_ap", "smooth", "AverageMeter"]
+
+# Training-side names of the reference's utils/util.py (losses, label assigner, EMA,
+# LR schedules, optimizer groups, plots, ONNX export, checkpoint stripping): outside
+# this build's scope. They exist here so the reference's module
+# surface is complete, and fail loudly when used.
+OUT_OF_SCOPE = ("Assigner", "BoxLoss", "ComputeLoss", "CosineLR", "EMA", "FocalLoss", "LinearLR", "QFL", "VFL",
+                "clip_gradients", "compute_iou", "export_onnx", "plot_curve", "plot_lr", "plot_pr_curve",
+                "set_params", "strip_optimizer")
+
+
+def _out_of_scope(name, ref):
+    def stub(*args, **kwargs):
+        raise NotImplementedError(f"utils.util.{name} ({ref} in the reference) is training-side and outside this "
+                                  f"inference build's scope; use the reference's own utils for training")
+    stub.__name__ = stub.__qualname__ = name
+    stub.__doc__ = f"Out of scope: the reference's {ref} (training side). Raises NotImplementedError."
+    return stub
+
+
+for _name, _ref in zip(OUT_OF_SCOPE, ("utils/util.py:643", "utils/util.py:798", "utils/util.py:831",
+                                      "utils/util.py:559", "utils/util.py:599", "utils/util.py:775",
+                                      "utils/util.py:581", "utils/util.py:738", "utils/util.py:749",
+                                      "utils/util.py:340", "utils/util.py:303", "utils/util.py:47",
+                                      "utils/util.py:202", "utils/util.py:537", "utils/util.py:180",
+                                      "utils/util.py:519", "utils/util.py:332")):
+    globals()[_name] = _out_of_scope(_name, _ref)
+del _name, _ref
+
+
+class AverageMeter:
+    """Running mean of per-batch values weighted by batch size, NaNs skipped
+    (reference utils/util.py:630-640; main.py:119-121 logs losses with it)."""
+
+    def __init__(self):
+        self.num = 0
+        self.sum = 0
+        self.avg = 0
+
+    def update(self, v, n):
+        if math.isnan(float(v)):
+            return
+        self.num += n
+        self.sum += v * n
+        self.avg = self.sum / self.num
 
 MAX_WH = 7680
 MAX_DET = 300
@@ -45,6 +91,22 @@ def setup_seed():
     torch.manual_seed(0)
     torch.backends.cudnn.benchmark = False
     torch.backends.cudnn.deterministic = True
+
+
+def setup_multi_processes():
+    """Process settings of the reference's entry point (utils/util.py:23-44, called by main.py:354):
+    the `fork` start method, OpenCV's own threading off when cv2 is installed, and OMP / MKL
+    thread counts of 1 unless the environment sets them."""
+    import platform
+    if platform.system() != "Windows":
+        torch.multiprocessing.set_start_method("fork", force=True)
+    try:
+        import cv2
+        cv2.setNumThreads(0)
+    except ImportError:
+        pass
+    os.environ.setdefault("OMP_NUM_THREADS", "1")
+    os.environ.setdefault("MKL_NUM_THREADS", "1")
 
 
 def wh2xy(x):

@@ -57,6 +57,10 @@ _PROTOS = {
                              POINTER(c_double), POINTER(c_int)]),
     "yh_nms_host": (c_int, [c_int, c_void_p, c_int, c_int, c_int, c_float, c_double, c_int, c_int, c_float,
                             c_void_p, c_void_p, c_int]),
+    "yh_letterbox_geometry": (c_int, [c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p]),
+    "yh_letterbox": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p]),
+    "yh_letterbox_host": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_int]),
+    "yh_resize_linear_host": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p]),
 }
 
 _lib = None

@@ -50,21 +50,39 @@ class Gather:
     Every rank must hold the same per-rank batch (the bench's weak-scaling case);
     for ragged shards pad the packed tensor to the largest shard and drop the
     padding rows on rank 0 with `shard()`.
+
+    Results land in a ring of `slots` buffer sets, one per call in turn, so a
+    pipelined caller (DetectPipeline, up to 2 x lanes batches in flight) can still
+    read batch k's gathered rows after batch k+1's gather has been queued; keep
+    `slots` at least the number of batches in flight.
+
+    With a torch.distributed process group the gather is always the collective
+    (RCCL on device tensors with backend "nccl", also at world size 1); without one
+    (plain single-process use) rank 0's own packed rows are returned.
     """
 
-    def __init__(self, batch, max_det, device, rank, world, group=None):
+    def __init__(self, batch, max_det, device, rank, world, group=None, slots=8):
         self.rank, self.world, self.group = rank, world, group
         self.batch, self.max_det = batch, max_det
-        self.bufs = ([torch.empty((batch, max_det * 6 + 1), dtype=torch.float32, device=device)
-                      for _ in range(world)] if rank == 0 else None)
+        self.slots = max(1, int(slots))
+        self.calls = 0
+        self.bufs = ([[torch.empty((batch, max_det * 6 + 1), dtype=torch.float32, device=device)
+                       for _ in range(world)] for _ in range(self.slots)] if rank == 0 else None)
 
     def __call__(self, dets, counts):
         """Collective: returns the list of per-rank packed tensors on rank 0, None elsewhere."""
         packed = pack(dets, counts)
-        if self.world == 1:
-            return [packed]
-        torch.distributed.gather(packed, self.bufs, dst=0, group=self.group)
-        return self.bufs if self.rank == 0 else None
+        slot = self.calls % self.slots
+        self.calls += 1
+        dist = torch.distributed.is_available() and torch.distributed.is_initialized()
+        if not dist:
+            if self.world != 1:
+                raise RuntimeError("Gather over several ranks needs an initialised process group")
+            self.bufs[slot][0].copy_(packed)
+            return self.bufs[slot]
+        out = self.bufs[slot] if self.rank == 0 else None
+        torch.distributed.gather(packed, out, dst=0, group=self.group)
+        return out
 
     def detections(self, gathered, total=None):
         """Rank 0: flatten gathered packed tensors into the global per-image list (rank order)."""

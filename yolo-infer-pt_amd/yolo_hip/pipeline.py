@@ -28,11 +28,25 @@ import torch
 from .engine import nms
 
 
+def _tensors(obj):
+    if isinstance(obj, torch.Tensor):
+        yield obj
+    elif isinstance(obj, (list, tuple)):
+        for o in obj:
+            yield from _tensors(o)
+
+
 class DetectPipeline:
-    """submit(x) -> (dets, counts) of that batch, valid once `wait(handle)` or a sync has run.
+    """submit(x) -> (dets, counts, extra, done) of that batch; read them on a stream after
+    `wait(done)` (or after a device sync).
 
     `post` (optional) is called on the NMS stream with (dets, counts) - e.g. the
-    data-parallel gather - and its return value is kept with the batch.
+    data-parallel gather - and its return value (`extra`) is kept with the batch.
+
+    Stream safety: dets / counts (and the tensors in `extra`) are allocated on the
+    NMS stream; submit() marks them used on the caller's stream (record_stream), so
+    once the caller drops them the caching allocator does not hand their blocks to a
+    later batch's NMS before the caller's queued reads have run.
     """
 
     def __init__(self, engine, batch, height, width, post=None, depth=2, nms_kwargs=None, nms_on_lane=False):
@@ -81,8 +95,17 @@ class DetectPipeline:
             done = torch.cuda.Event()
             done.record(ns)
         self.free[i] = done
-        # the results were allocated on the NMS stream; the caller reads them after `done`
+        # allocated on the NMS stream, read on the caller's: keep the blocks out of the
+        # NMS stream's free pool until the caller's work queued after `done` has run
+        if ns is not main:
+            for t in (dets, counts, *_tensors(extra)):
+                if t.is_cuda:
+                    t.record_stream(main)
         return dets, counts, extra, done
+
+    def wait(self, done):
+        """Make the caller's stream wait for one submitted batch's NMS (+ post)."""
+        torch.cuda.current_stream(self.eng.device).wait_event(done)
 
     def drain(self):
         """Make the caller's stream wait for every NMS in flight."""
