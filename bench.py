@@ -217,11 +217,7 @@ def main():
     from yolo_hip.engine import Engine, nms
     from yolo_hip.pipeline import DetectPipeline
 
-    if args.lanes > 1 and not args.serial:
-        # The lanes supply the concurrency the segment split (YH_HEADSPLIT, a second stream
-        # per engine) would: keep lanes + the NMS stream within the 4 HIP hardware queues.
-        os.environ.setdefault("YH_HEADSPLIT", "0")
-    else:
+    if args.serial:
         args.lanes = 1
     model = build_model(args.variant)
     eng = Engine(*model._yh_arch, dev, dtype)

@@ -1,0 +1,53 @@
+"""Fused launches (csrc/head.hip) are bit-identical to the per-layer launches they replace.
+Marked gpu.
+
+The fused op recomputes the same layers in the same arithmetic order (per-channel depthwise
+FMA chains, conv_mx's K order on v_mfma_f32_32x32x16, one rounding per layer output), so the
+head output must be exactly equal with fusion on (default) and off (YH_FUSE=0 at handle
+creation), for every shape: whole and partial tiles, every level, both 16-bit dtypes.
+"""
+import os
+
+import pytest
+import torch
+
+from _util import make_model
+from yolo_hip import synth
+
+pytestmark = pytest.mark.gpu
+
+
+def _engine(model, dtype, dev, fuse):
+    from yolo_hip.engine import Engine
+    old = os.environ.get("YH_FUSE")
+    os.environ["YH_FUSE"] = "1" if fuse else "0"
+    try:
+        eng = Engine(*model._yh_arch, dev, dtype)
+    finally:
+        if old is None:
+            del os.environ["YH_FUSE"]
+        else:
+            os.environ["YH_FUSE"] = old
+    eng.load_module(model)
+    return eng
+
+
+@pytest.mark.parametrize("variant,dtype,batch,h,w", [("n", torch.bfloat16, 4, 640, 640), ("n", torch.float16, 2, 320, 256),
+                                                     ("s", torch.bfloat16, 2, 384, 640), ("x", torch.bfloat16, 1, 320, 320)])
+def test_fused_head_equals_per_layer_launches(gpu, variant, dtype, batch, h, w):
+    model = make_model(variant)
+    x = synth.synth_scenes(batch, h, w, seed=31).to(gpu, dtype)
+    fused = _engine(model, dtype, gpu, True)
+    plain = _engine(model, dtype, gpu, False)
+    kinds_f = {o["cls"] for o in fused.ops(batch, h, w)}
+    kinds_p = {o["cls"] for o in plain.ops(batch, h, w)}
+    assert "head_cls" not in kinds_p
+    if variant in ("n", "s"):   # x's cls branch (384 channels) keeps the per-layer launches
+        assert "head_cls" in kinds_f
+        assert len(fused.ops(batch, h, w)) < len(plain.ops(batch, h, w))
+    yf = fused.forward(x).clone()
+    yp = plain.forward(x).clone()
+    assert torch.isfinite(yf.float()).all()
+    assert torch.equal(yf, yp), (yf.float() - yp.float()).abs().max().item()
+    fused.set_graph(False)
+    assert torch.equal(fused.forward(x), yp)

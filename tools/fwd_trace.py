@@ -22,8 +22,6 @@ sys.path.insert(0, os.path.join(ROOT, "yolo-infer-pt_amd"))
 from yolo_hip import synth  # noqa: E402
 from yolo_hip.engine import Engine  # noqa: E402
 
-os.environ.setdefault("YH_HEADSPLIT", "0")   # one stream: dispatch order = op order
-
 DT = {"bf16": torch.bfloat16, "fp16": torch.float16, "fp32": torch.float32}
 
 

@@ -96,20 +96,38 @@ struct NmsArgs {
     unsigned long long* trace;  // optional [B][16] phase timestamps (s_memrealtime), nullptr = off
 };
 
-// Dense-conv kernels (16-bit types; F32 always runs conv_gemm). All of them
-// accumulate the K reduction in the same order (32-deep MFMA steps, increasing
-// k), so they produce bit-identical outputs and the engine may pick per layer.
-enum ConvKernel {
-    CONV_GEMM = 0,     // conv_gemm2, BM from the engine's tile heuristic
-    CONV_GEMM64 = 1,   // conv_gemm2, BM 64
-    CONV_GEMM128 = 2,  // conv_gemm2, BM 128
-    CONV_STREAM = 3,   // conv_stream, persistent BM 64 ring
-    CONV_DIRECT = 4,   // conv_direct, LDS-resident weights, register-streamed pixels
-    CONV_STREAM4 = 5,  // conv_stream, 4-slot ring (3 K stages in flight)
-    CONV_STREAM8 = 6,  // conv_stream, 8-slot ring (7 K stages in flight)
-    CONV_TINY = 7,     // conv_tiny, 3x3 stride 1 with Cin <= 32: input rows staged in LDS
-    CONV_NKERNELS = 8
+// Dense-conv kernel of the fp32 handle (conv.hip). The 16-bit handles run the
+// conv_mx family (conv_mx.h).
+enum ConvKernel { CONV_GEMM = 0 };
+
+// Fused cls branch of the detect head (nets/nn.py:244-252), one launch for all levels:
+//   DWConv 3x3 + SiLU -> Conv 1x1 + SiLU -> DWConv 3x3 + SiLU -> Conv 1x1 + SiLU
+//   -> Conv2d 1x1 (+ bias)
+// per TH x TW output tile, every intermediate in LDS (halo recomputed), bit-identical
+// to the five separate launches (same per-channel FMA order, same MFMA K order, one
+// rounding to the handle dtype per layer output).
+struct HeadClsLevel {
+    const void* x; int ldx, C0;      // level input (NHWC view), channels
+    int H, W;
+    void* y; int ldy;                // output view (the head tensor's cls slice)
+    const float* dw1w; const float* dw1b; int dw1ld;   // [9][dw1ld] fp32, bias
+    const void* pw1w; int pw1ld; const float* pw1b;    // [rows][pw1ld] dtype, bias
+    const float* dw2w; const float* dw2b; int dw2ld;
+    const void* pw2w; int pw2ld; const float* pw2b;
+    const void* pw3w; int pw3ld; const float* pw3b;
+    int TH, TW, ntw, tiles;          // output tile, tiles per row, tiles per image
+    int wg0;                         // first workgroup of the level (one workgroup per tile)
 };
+struct HeadClsArgs {
+    HeadClsLevel lv[3];
+    int nlv, B, c3, nc;
+    int dbg;                         // experiments (YH_HCLS_DBG): bit k skips phase k (0 dw1 .. 4 pw3)
+};
+constexpr int HEAD_CLS_THREADS = 256;
+constexpr int HEAD_CLS_LDS = 40 * 1024;    // four workgroups (16 waves) per CU
+// LDS bytes of a tile's buffers; 0 if it does not fit
+int head_cls_lds(int TH, int TW, int C0, int c3, int nc);
+int launch_head_cls(int dtype, const HeadClsArgs& a, hipStream_t s);
 
 // launchers (return hipError_t as int)
 bool conv_kernel_ok(int dtype, int kern, const ConvArgs& a);

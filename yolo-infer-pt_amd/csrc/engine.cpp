@@ -89,8 +89,9 @@ static uint16_t f2h(float f) {
 
 // ---------------------------------------------------------------- graph model
 enum ConvKind { CK_DENSE = 0, CK_FIRST = 1, CK_DW = 2, CK_PE = 3 };
-enum OpKind { OP_FIRST, OP_CONV, OP_DW, OP_SPPF, OP_ATTN, OP_DECODE };
-enum OpClass { CL_CONV3 = 0, CL_CONV1 = 1, CL_FIRST = 2, CL_DW = 3, CL_SPPF = 4, CL_ATTN = 5, CL_DECODE = 6, CL_N = 7 };
+enum OpKind { OP_FIRST, OP_CONV, OP_DW, OP_SPPF, OP_ATTN, OP_DECODE, OP_HEADCLS };
+enum OpClass { CL_CONV3 = 0, CL_CONV1 = 1, CL_FIRST = 2, CL_DW = 3, CL_SPPF = 4, CL_ATTN = 5, CL_DECODE = 6,
+               CL_HEADCLS = 7, CL_N = 8 };
 
 struct Tensor { int level; int C; };        // physical channels = pixel stride
 struct View { int t = -1; int coff = 0; int C = 0; };
@@ -120,6 +121,11 @@ struct Op {
     bool has_res = false;
     int heads = 0;
     View lvl[3];
+    // OP_HEADCLS: per level (index = detect level 0..2) the five convs of the cls branch
+    // (dw1, pw1, dw2, pw2, pw3), the level input and the head tensor's cls slice
+    int hc[3][5] = {};
+    View hx[3], hy[3];
+    bool hlv[3] = {false, false, false};   // levels the fused op covers
     std::string label;
 };
 
@@ -370,6 +376,12 @@ struct Net {
         // per level, coarsest first: the 20x20 and 40x40 head branches join the
         // level program that computes P5 / P4; the 80x80 level runs last
         for (int l = 0; l < 3; ++l) L[l] = tensor(3 + l, 64 + ncp);
+        // 16-bit handles run the three cls branches as one fused launch (head.hip) when
+        // every level has an LDS tile; YH_FUSE=0 keeps the per-layer launches
+        bool fuse_any = false;
+        Op hcop;
+        hcop.kind = OP_HEADCLS;
+        hcop.label = "head.cls";
         for (int l : {2, 1, 0}) {
             const int lvl = 3 + l;
             const std::string bp = "head.box." + std::to_string(l);
@@ -378,17 +390,30 @@ struct Net {
             conv3(bp + ".1", full(tb1, boxc), boxc, boxc, 1, ACT_SILU, full(tb2, boxc));
             dense(bp + ".2", {Seg{full(tb2, boxc), 0}}, {boxc}, 64, 1, 1, ACT_ID, slice(L[l], 0, 64), nullptr, 1);
             const std::string cp = "head.cls." + std::to_string(l);
+            View o;
+            o.t = L[l];
+            o.coff = 64;
+            o.C = ncp;
+            if (fuse_head_cls(xc[l], clsc, nc)) {
+                // the same five convs (weights are loaded by name), no per-layer ops
+                fuse_any = hcop.hlv[l] = true;
+                hcop.hc[l][0] = new_conv(cp + ".0", CK_DW, xc[l], xc[l], 3, 1, xc[l], 0, ACT_SILU);
+                hcop.hc[l][1] = new_dense_conv(cp + ".1", xc[l], clsc, 1, 0, ACT_SILU);
+                hcop.hc[l][2] = new_conv(cp + ".2", CK_DW, clsc, clsc, 3, 1, clsc, 0, ACT_SILU);
+                hcop.hc[l][3] = new_dense_conv(cp + ".3", clsc, clsc, 1, 0, ACT_SILU);
+                hcop.hc[l][4] = new_dense_conv(cp + ".4", clsc, nc, 1, 1, ACT_ID);
+                hcop.hx[l] = full(xs[l], xc[l]);
+                hcop.hy[l] = o;
+                continue;
+            }
             const int tc1 = tensor(lvl, xc[l]), tc2 = tensor(lvl, clsc), tc3 = tensor(lvl, clsc), tc4 = tensor(lvl, clsc);
             dw(cp + ".0", full(xs[l], xc[l]), xc[l], full(tc1, xc[l]));
             conv1(cp + ".1", full(tc1, xc[l]), xc[l], clsc, ACT_SILU, full(tc2, clsc));
             dw(cp + ".2", full(tc2, clsc), clsc, full(tc3, clsc));
             conv1(cp + ".3", full(tc3, clsc), clsc, clsc, ACT_SILU, full(tc4, clsc));
-            View o;
-            o.t = L[l];
-            o.coff = 64;
-            o.C = ncp;
             dense(cp + ".4", {Seg{full(tc4, clsc), 0}}, {clsc}, nc, 1, 1, ACT_ID, o, nullptr, 1);
         }
+        if (fuse_any) ops.push_back(hcop);
         Op dec;
         dec.kind = OP_DECODE;
         for (int l = 0; l < 3; ++l) dec.lvl[l] = full(L[l]);
@@ -396,6 +421,36 @@ struct Net {
         ops.push_back(dec);
         finalize_convs();
     }
+    // a dense conv with a single unsegmented input and no op of its own (fused ops)
+    int new_dense_conv(const std::string& name, int cin, int cout, int k, int has_bias, int act) {
+        const int ci = new_conv(name, CK_DENSE, cin, cout, k, 1, 1, has_bias, act);
+        convs[ci].segs.push_back({cin, round_up(cin, 8)});
+        return ci;
+    }
+    // a level's cls branch is fused when it has 16-channel blocks, 4-channel class groups
+    // and an LDS tile next to its resident weights
+    bool fuse_head_cls(int C0, int c3, int nc) const {
+        const char* e = getenv("YH_FUSE");
+        if (dtype == F32 || (e && atoi(e) == 0)) return false;
+        if (c3 % 16 || nc % 4 || C0 % 16) return false;
+        int TH, TW;
+        return head_cls_tile(C0, c3, nc, 1 << 30, 1 << 30, TH, TW);
+    }
+    // output tile of one level of the fused cls branch: the largest candidate whose
+    // workgroup (resident weights + one tile's buffers) fits the LDS
+    static bool head_cls_tile(int C0, int c3, int nc, int H, int W, int& TH, int& TW) {
+        static const int cand[][2] = {{8, 16}, {8, 8}, {4, 16}, {4, 8}, {8, 4}, {4, 4}, {2, 8}, {2, 4}, {2, 2}};
+        for (auto& c : cand) {
+            if (c[0] > H || c[1] > W) continue;
+            if (head_cls_lds(c[0], c[1], C0, c3, nc) > 0) {
+                TH = c[0];
+                TW = c[1];
+                return true;
+            }
+        }
+        return false;
+    }
+
     void dw(const std::string& name, View x, int ch, View out) {
         const int ci = new_conv(name, CK_DW, ch, ch, 3, 1, ch, 0, ACT_SILU);
         Op op;
@@ -774,6 +829,57 @@ struct Net {
         (void)hipEventDestroy(e1);
     }
 
+    HeadClsArgs head_cls_args(const Op& op, int B, int H, int W) {
+        HeadClsArgs a{};
+        a.B = B;
+        a.nc = var.num_classes;
+        a.c3 = convs[op.hc[0][1]].cout;
+        // one persistent workgroup per CU, split over the levels by estimated work
+        double cost[3], total = 0;
+        int lvls[3], nl = 0;
+        for (int l = 0; l < 3; ++l)
+            if (op.hlv[l]) lvls[nl++] = l;
+        for (int k = 0; k < nl; ++k) {
+            const int l = lvls[k];
+            HeadClsLevel& v = a.lv[a.nlv++];
+            const Tensor& t = tensors[op.hx[l].t];
+            v.H = H >> t.level;
+            v.W = W >> t.level;
+            v.x = ptr(op.hx[l]);
+            v.ldx = ldc(op.hx[l]);
+            v.C0 = op.hx[l].C;
+            v.y = ptr(op.hy[l]);
+            v.ldy = ldc(op.hy[l]);
+            const ConvDesc &d1 = convs[op.hc[l][0]], &p1 = convs[op.hc[l][1]], &d2 = convs[op.hc[l][2]],
+                           &p2 = convs[op.hc[l][3]], &p3 = convs[op.hc[l][4]];
+            require(d1.loaded && p1.loaded && d2.loaded && p2.loaded && p3.loaded, "head.cls weights not loaded");
+            v.dw1w = (const float*)d1.w_dev; v.dw1b = d1.b_dev; v.dw1ld = d1.cout_p;
+            v.pw1w = p1.w_dev; v.pw1ld = p1.Kp; v.pw1b = p1.b_dev;
+            v.dw2w = (const float*)d2.w_dev; v.dw2b = d2.b_dev; v.dw2ld = d2.cout_p;
+            v.pw2w = p2.w_dev; v.pw2ld = p2.Kp; v.pw2b = p2.b_dev;
+            v.pw3w = p3.w_dev; v.pw3ld = p3.Kp; v.pw3b = p3.b_dev;
+            require(head_cls_tile(v.C0, a.c3, a.nc, v.H, v.W, v.TH, v.TW), "head.cls: no LDS tile");
+            v.ntw = (v.W + v.TW - 1) / v.TW;
+            v.tiles = v.ntw * ((v.H + v.TH - 1) / v.TH);
+            const double mp = (v.TH + 2.0) * (v.TW + 2.0), no = (double)v.TH * v.TW;
+            const double c3p = 32.0 * ((a.c3 + 31) / 32), ncp = 32.0 * ((a.nc + 31) / 32);
+            // MACs per tile (depthwise VALU weighted 4x an MFMA MAC) + the input tile's bytes
+            cost[k] = (double)B * v.tiles *
+                      (mp * v.C0 * (36.0 + c3p) + no * a.c3 * (36.0 + c3p + ncp) +
+                       64.0 * (v.TH + 4.0) * (v.TW + 4.0) * v.C0);
+            total += cost[k];
+        }
+        if (const char* e = getenv("YH_HCLS_DBG")) a.dbg = atoi(e);
+        // one workgroup per tile, the 80x80 level (most work) first
+        int wg = 0;
+        for (int k = 0; k < nl; ++k) {
+            a.lv[k].wg0 = wg;
+            wg += B * a.lv[k].tiles;
+        }
+        (void)cost; (void)total;
+        return a;
+    }
+
     void launch_op(size_t oi, int B, int H, int W, hipStream_t s) {
         const Op& op = ops[oi];
         int rc = 0;
@@ -809,6 +915,7 @@ struct Net {
             case OP_DW: rc = launch_dwconv(dtype, dw_args(op, B, H, W), s); break;
             case OP_SPPF: rc = launch_sppf(dtype, pool_args(op, B, H, W), s); break;
             case OP_ATTN: rc = launch_attention(dtype, attn_args(op, H, W), B, s); break;
+            case OP_HEADCLS: rc = launch_head_cls(dtype, head_cls_args(op, B, H, W), s); break;
             case OP_DECODE: {
                 DecodeArgs a{};
                 for (int l = 0; l < 3; ++l) {
@@ -856,134 +963,6 @@ struct Net {
                 if (e != hipSuccess) throw Fail(YH_EHIP, "unit " + ops[u.first].label + ": " + hipGetErrorString(e));
             }
         }
-    }
-
-    // ---------------------------------------------------------- unit dependencies
-    struct Rg { int t, c0, c1; };
-    void unit_regions(const Unit& u, std::vector<Rg>& rd, std::vector<Rg>& wr) const {
-        for (int k = u.first; k < u.last; ++k) {
-            const Op& op = ops[k];
-            for (auto& sg : op.in) rd.push_back({sg.v.t, sg.v.coff, sg.v.coff + sg.v.C});
-            if (op.has_res) rd.push_back({op.res.t, op.res.coff, op.res.coff + op.res.C});
-            if (op.kind == OP_DECODE) {
-                for (int l = 0; l < 3; ++l) rd.push_back({op.lvl[l].t, 0, tensors[op.lvl[l].t].C});
-                wr.push_back({-2, 0, 1});   // the caller's y
-            } else if (op.kind == OP_SPPF) {
-                rd.push_back({op.out.t, op.out.coff, op.out.coff + op.out.C});
-                wr.push_back({op.out.t, op.out.coff + op.out.C, op.out.coff + 4 * op.out.C});
-            } else {
-                wr.push_back({op.out.t, op.out.coff, op.out.coff + op.out.C});
-            }
-            if (op.kind == OP_FIRST) rd.push_back({-1, 0, 1});   // the caller's x
-        }
-    }
-
-    // ---------------------------------------------------------- segment split
-    // The forward is replayed as four single-chain graphs on two streams, joined by
-    // events between launches (no multi-branch graph: see par_streams):
-    //   A  backbone + FPN top-down (through fpn.h2, which produces P3')   stream 0
-    //   B  the 80x80 detect head (head.box.0.*, head.cls.0.*)             stream 1, after A
-    //   C  FPN bottom-up (fpn.h3 ..) + the 40x40 / 20x20 heads           stream 0
-    //   D  decode                                                         stream 0, after B
-    // B is throughput work (the largest head level) and C is a chain of small,
-    // latency-bound layers, so B fills the CUs C leaves idle. The split is checked
-    // against the channel-range dependencies of every unit. YH_HEADSPLIT=0 turns it off.
-    bool head_split = [] { const char* e = getenv("YH_HEADSPLIT"); return !e || atoi(e) != 0; }();
-    hipStream_t hs_stream = nullptr;
-    hipEvent_t hs_ev[3] = {nullptr, nullptr, nullptr};
-    // segment of each unit (0 A, 1 B, 2 C, 3 D) if the plan splits cleanly, else empty
-    // happens-before between segments under forward_head_split's launch order
-    //   s0: A(0) -eA-> C1(2) -eC-> C3(4) -(wait eB)-> D(5);  s1: (wait eA) B0(1) (wait eC) B1(3) -eB->
-    static bool seg_before(int a, int b) {
-        static const bool hb[6][6] = {
-            {0, 1, 1, 1, 1, 1}, {0, 0, 0, 1, 0, 1}, {0, 0, 0, 1, 1, 1},
-            {0, 0, 0, 0, 0, 1}, {0, 0, 0, 0, 0, 1}, {0, 0, 0, 0, 0, 0}};
-        return hb[a][b];
-    }
-    std::vector<int> head_segments() const {
-        const auto& us = cur_plan->units;
-        const int n = (int)us.size();
-        std::vector<int> seg(n, -1);
-        int last_h2 = -1, last_h4 = -1;
-        for (int j = 0; j < n; ++j) {
-            const Unit& u = us[j];
-            const std::string& lb = ops[u.first].label;
-            auto pre = [&](const char* x) { return lb.rfind(x, 0) == 0; };
-            const bool h0 = pre("head.box.0.") || pre("head.cls.0."), h1 = pre("head.box.1.") || pre("head.cls.1.");
-            const bool dec = ops[u.first].kind == OP_DECODE;
-            for (int k = u.first; k < u.last; ++k) {
-                if (ops[k].label.rfind("fpn.h2", 0) == 0) last_h2 = j;
-                if (ops[k].label.rfind("fpn.h4", 0) == 0) last_h4 = j;
-            }
-            seg[j] = h0 ? 1 : h1 ? 3 : dec ? 5 : -1;
-        }
-        if (last_h2 < 0 || last_h4 < last_h2 || seg[n - 1] != 5) return {};
-        for (int j = 0; j < n; ++j)
-            if (seg[j] < 0) seg[j] = j <= last_h2 ? 0 : j <= last_h4 ? 2 : 4;
-        for (int j = 0; j < n - 1; ++j)
-            if (seg[j] == 5) return {};
-        // every dependency must follow the segments' happens-before order
-        std::vector<std::vector<Rg>> rd(n), wr(n);
-        for (int j = 0; j < n; ++j) unit_regions(us[j], rd[j], wr[j]);
-        auto ov = [](const std::vector<Rg>& a, const std::vector<Rg>& b) {
-            for (auto& x : a)
-                for (auto& y : b)
-                    if (x.t == y.t && x.c0 < y.c1 && y.c0 < x.c1) return true;
-            return false;
-        };
-        for (int j = 0; j < n; ++j)
-            for (int i = 0; i < j; ++i) {
-                if (!(ov(wr[i], rd[j]) || ov(rd[i], wr[j]) || ov(wr[i], wr[j]))) continue;
-                if (seg[i] != seg[j] && !seg_before(seg[i], seg[j])) return {};
-            }
-        return seg;
-    }
-    hipGraphExec_t capture_segment(const std::vector<int>& seg, int which, int B, int H, int W) {
-        if (!cap_stream) HIPCHECK(hipStreamCreateWithFlags(&cap_stream, hipStreamNonBlocking));
-        hipGraph_t g = nullptr;
-        HIPCHECK(hipStreamBeginCapture(cap_stream, hipStreamCaptureModeThreadLocal));
-        try {
-            for (size_t j = 0; j < seg.size(); ++j)
-                if (seg[j] == which) launch_unit(cur_plan->units[j], B, H, W, cap_stream);
-        } catch (...) {
-            (void)hipStreamEndCapture(cap_stream, &g);
-            if (g) (void)hipGraphDestroy(g);
-            throw;
-        }
-        HIPCHECK(hipStreamEndCapture(cap_stream, &g));
-        hipGraphExec_t ex = nullptr;
-        HIPCHECK(hipGraphInstantiate(&ex, g, nullptr, nullptr, 0));
-        (void)hipGraphDestroy(g);
-        return ex;
-    }
-    // true if the forward was launched as the four head-split graphs
-    bool forward_head_split(int B, int H, int W, hipStream_t s) {
-        GraphKey k0{B, H, W, in_u8 | 2};
-        auto it = graphs.find(k0);
-        if (it == graphs.end()) {
-            const std::vector<int> seg = head_segments();
-            if (seg.empty()) return false;
-            run_ops(B, H, W, s);   // eager pass: first launches outside any capture
-            for (int w = 0; w < 6; ++w)
-                graphs.emplace(GraphKey{B, H, W, in_u8 | ((w + 1) << 1)}, capture_segment(seg, w, B, H, W));
-            if (!hs_stream) HIPCHECK(hipStreamCreateWithFlags(&hs_stream, hipStreamNonBlocking));
-            for (auto& e : hs_ev)
-                if (!e) HIPCHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-        }
-        auto g = [&](int w) { return graphs.at(GraphKey{B, H, W, in_u8 | ((w + 1) << 1)}); };
-        HIPCHECK(hipGraphLaunch(g(0), s));              // A: backbone + FPN top-down
-        HIPCHECK(hipEventRecord(hs_ev[0], s));
-        HIPCHECK(hipStreamWaitEvent(hs_stream, hs_ev[0], 0));
-        HIPCHECK(hipGraphLaunch(g(1), hs_stream));      // B0: 80x80 head
-        HIPCHECK(hipGraphLaunch(g(2), s));              // C1: fpn.h3, fpn.h4
-        HIPCHECK(hipEventRecord(hs_ev[1], s));
-        HIPCHECK(hipStreamWaitEvent(hs_stream, hs_ev[1], 0));
-        HIPCHECK(hipGraphLaunch(g(3), hs_stream));      // B1: 40x40 head
-        HIPCHECK(hipEventRecord(hs_ev[2], hs_stream));
-        HIPCHECK(hipGraphLaunch(g(4), s));              // C3: fpn.h5, fpn.h6, 20x20 head
-        HIPCHECK(hipStreamWaitEvent(s, hs_ev[2], 0));
-        HIPCHECK(hipGraphLaunch(g(5), s));              // D: decode
-        return true;
     }
 
     void run_ops(int B, int H, int W, hipStream_t s) {
@@ -1041,7 +1020,6 @@ struct Net {
             run_ops(B, H, W, s);
             return;
         }
-        if (head_split && forward_head_split(B, H, W, s)) return;
         const GraphKey key{B, H, W, in_u8};
         auto it = graphs.find(key);
         if (it == graphs.end()) {
@@ -1079,6 +1057,7 @@ struct Net {
             case OP_SPPF: return CL_SPPF;
             case OP_ATTN: return CL_ATTN;
             case OP_DECODE: return CL_DECODE;
+            case OP_HEADCLS: return CL_HEADCLS;
         }
         return CL_CONV1;
     }
@@ -1126,6 +1105,20 @@ struct Net {
                 flops = (double)B * op.heads * (2.0 * T * T * (32 + 64)) + 2.0 * B * T * C * 9;
                 break;
             }
+            case OP_HEADCLS: {
+                // the level inputs read once, the class logits written once, weights once
+                for (int l = 0; l < 3; ++l) {
+                    if (!op.hlv[l]) continue;
+                    const double n = px(tensors[op.hx[l].t].level);
+                    const int C0 = op.hx[l].C;
+                    const ConvDesc& p1 = convs[op.hc[l][1]];
+                    const int c3 = p1.cout, nc = convs[op.hc[l][4]].cout;
+                    bytes += n * C0 * es + n * nc * es + (9.0 * (C0 + c3) * 4) +
+                             ((double)C0 * c3 + (double)c3 * c3 + (double)c3 * nc) * es;
+                    flops += 2.0 * n * (9.0 * C0 + (double)C0 * c3 + 9.0 * c3 + (double)c3 * c3 + (double)c3 * nc);
+                }
+                break;
+            }
             case OP_DECODE: {
                 double A = 0, cin = 0;
                 for (int l = 0; l < 3; ++l) {
@@ -1148,9 +1141,6 @@ struct Net {
         if (io_dev) (void)hipFree(io_dev);
         if (zero_dev) (void)hipFree(zero_dev);
         if (cap_stream) (void)hipStreamDestroy(cap_stream);
-        if (hs_stream) (void)hipStreamDestroy(hs_stream);
-        for (auto e : hs_ev)
-            if (e) (void)hipEventDestroy(e);
         for (auto e : ev) (void)hipEventDestroy(e);
     }
 };
@@ -1423,7 +1413,7 @@ int yh_op_kernel(const yh_handle* h, int index, int batch, int height, int width
     return guarded([&] {
         yh::require(h && index >= 0 && index < (int)h->net.ops.size(), "op index out of range");
         const yh::Net& n = h->net;
-        static const char* op_names[] = {"stem", "conv", "dwconv", "sppf", "attention", "decode"};
+        static const char* op_names[] = {"stem", "conv", "dwconv", "sppf", "attention", "decode", "head_cls"};
         const yh::Op& op = n.ops[index];
         if (op.kind != yh::OP_CONV) {
             if (name) *name = op_names[(int)op.kind];

@@ -1,0 +1,308 @@
+// Fused detect-head branches (16-bit handles).
+//
+//   head_cls   the cls branch of every level (nets/nn.py:244-252: DWConv 3x3 -> Conv 1x1
+//              -> DWConv 3x3 -> Conv 1x1 -> Conv2d 1x1) in one launch. A workgroup owns a
+//              TH x TW output tile of one image of one level; the input tile with a 2-pixel
+//              halo, the first depthwise output and first pointwise output with a 1-pixel
+//              halo, the second depthwise and pointwise outputs all stay in LDS; only the
+//              level input is read from HBM and only the nc class logits are written.
+//
+// Bit-identical to the unfused launches: the depthwise convs run dwconv3x3_c4's per-channel
+// FMA chain (taps row-major, fp32, + bias, SiLU, one rounding), the pointwise convs run
+// conv_mx's K order (16-channel blocks ascending, one v_mfma_f32_32x32x16 step each, fp32
+// accumulator, + bias, activation, one rounding). The first pointwise output is zeroed
+// outside the image: it is the second depthwise conv's zero padding.
+#include "common.h"
+#include "dtypes.h"
+
+namespace yh {
+
+namespace {
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+template <typename T> struct HMfma;
+template <> struct HMfma<__bf16> {
+    static __device__ __forceinline__ f32x16 step(const uint4& a, const uint4& b, const f32x16& c) {
+        return __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, a), __builtin_bit_cast(bf16x8, b), c, 0,
+                                                       0, 0);
+    }
+};
+template <> struct HMfma<_Float16> {
+    static __device__ __forceinline__ f32x16 step(const uint4& a, const uint4& b, const f32x16& c) {
+        return __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(f16x8, a), __builtin_bit_cast(f16x8, b), c, 0, 0,
+                                                      0);
+    }
+};
+
+constexpr int NWV = HEAD_CLS_THREADS / 64;
+
+// Workgroup barrier for LDS hand-offs only: __syncthreads() also waits for every global
+// load in flight (vmcnt(0)), which would drain the weight loads issued ahead of a phase.
+__device__ __forceinline__ void hc_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+constexpr int HC_CK = 64;    // input channels staged per pass (the first depthwise conv's chunk)
+constexpr int HC_RB = 4;     // output rows per depthwise item (register sliding window)
+
+// LDS of one tile: region 1 = the input chunk (XH x XW x min(C0, HC_CK)), later the first /
+// second pointwise outputs; region 2 = the first / second depthwise outputs
+struct HcLayout {
+    int SX, SD, SM, r1, total;
+};
+__host__ __device__ inline HcLayout hc_layout(int TH, int TW, int C0, int c3) {
+    HcLayout L;
+    const int ck = C0 < HC_CK ? C0 : HC_CK;
+    L.SX = ck + 8; L.SD = C0 + 8; L.SM = c3 + 8;
+    const int MP = (TH + 2) * (TW + 2), NO = TH * TW;
+    const int x = (TH + 4) * (TW + 4) * L.SX * 2, p1 = MP * L.SM * 2, p2 = NO * L.SM * 2;
+    const int d1 = MP * L.SD * 2, d2 = NO * L.SM * 2;
+    int a = x > p1 ? x : p1;
+    a = a > p2 ? a : p2;
+    L.r1 = (a + 15) & ~15;
+    L.total = L.r1 + (d1 > d2 ? d1 : d2);
+    return L;
+}
+
+// Depthwise 3x3 + bias + SiLU over channels [c_lo, c_lo + C) of region `src` (row width SW
+// pixels, stride ss, channel offset 0 = c_lo) into `dst` (DH x DW pixels, stride ds, channel
+// offset c_lo). An item is (4-channel group, column, block of HC_RB rows): its (HC_RB + 2) x 3
+// input pixels are read once and every output row has its own FMA chain (taps row-major).
+template <typename T>
+__device__ __forceinline__ void hc_dw(const T* src, int SW, int ss, T* dst, int DH, int DW, int ds, int c_lo, int C,
+                                      const float* w, int wld, const float* b) {
+    const int nrb = (DH + HC_RB - 1) / HC_RB, per_g = DW * nrb, ng = C >> 2;
+    // the first item's weights are loaded before the barrier that opens the phase
+    float4 wt[9], bb;
+    int wg = -1;
+    auto load_w = [&](int g) {
+        const int c0 = c_lo + g * 4;
+#pragma unroll
+        for (int k = 0; k < 9; ++k) wt[k] = *reinterpret_cast<const float4*>(w + k * wld + c0);
+        bb = *reinterpret_cast<const float4*>(b + c0);
+        wg = g;
+    };
+    if ((int)threadIdx.x < ng * per_g) load_w(threadIdx.x / per_g);
+    hc_barrier();   // src complete
+    for (int q = threadIdx.x; q < ng * per_g; q += HEAD_CLS_THREADS) {
+        const int g = q / per_g, rem = q - g * per_g;
+        const int rb = rem / DW, c = rem - rb * DW;
+        const int r0 = rb * HC_RB, c0 = c_lo + g * 4;
+        if (g != wg) load_w(g);
+        uint2 xv[HC_RB + 2][3];
+#pragma unroll
+        for (int r = 0; r < HC_RB + 2; ++r)
+#pragma unroll
+            for (int kw = 0; kw < 3; ++kw) {
+                const int rr = min(r0 + r, DH + 1);
+                xv[r][kw] = *reinterpret_cast<const uint2*>(src + (rr * SW + c + kw) * ss + g * 4);
+            }
+#pragma unroll
+        for (int o = 0; o < HC_RB; ++o) {
+            if (r0 + o >= DH) break;
+            float acc[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int kh = 0; kh < 3; ++kh)
+#pragma unroll
+                for (int kw = 0; kw < 3; ++kw) {
+                    const T* xe = reinterpret_cast<const T*>(&xv[o + kh][kw]);
+                    const float4 wk = wt[kh * 3 + kw];
+                    acc[0] = fmaf(wk.x, tof(xe[0]), acc[0]);
+                    acc[1] = fmaf(wk.y, tof(xe[1]), acc[1]);
+                    acc[2] = fmaf(wk.z, tof(xe[2]), acc[2]);
+                    acc[3] = fmaf(wk.w, tof(xe[3]), acc[3]);
+                }
+            T o4[4];
+            o4[0] = fromf<T>(silu<T>(acc[0] + bb.x));
+            o4[1] = fromf<T>(silu<T>(acc[1] + bb.y));
+            o4[2] = fromf<T>(silu<T>(acc[2] + bb.z));
+            o4[3] = fromf<T>(silu<T>(acc[3] + bb.w));
+            *reinterpret_cast<uint2*>(dst + ((r0 + o) * DW + c) * ds + c0) = *reinterpret_cast<const uint2*>(o4);
+        }
+    }
+}
+
+// Pointwise conv phase: A = weights [rows][wld] (dtype, global; rows >= na * 32 zero-padded)
+// times the NPX pixels of LDS `src` (stride ss, 16 NK channels). The A fragments of the first
+// 32-cout tile are loaded before the barrier that opens the phase (they do not depend on
+// LDS), the next tile's while the current one's MFMAs run. Each wave takes 32-pixel B tiles
+// round-robin (B fragments read once per B tile). K order: 16-channel blocks ascending.
+// store(px, co, 4 rounded values) for couts co < M.
+template <typename T, int NK, typename Store>
+__device__ __forceinline__ void hc_pw_k(const T* src, int ss, int NPX, const T* w, int wld, const float* bias, int M,
+                                        bool silu_act, Store store) {
+    constexpr int NA_MAX = 4;
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int l32 = lane & 31, h = lane >> 5;
+    const int na = (M + 31) >> 5, nb = (NPX + 31) >> 5;
+    uint4 af[2][NK];   // A fragments of couts tiles a (af[a & 1]) and a + 1
+    auto load_a = [&](int a, uint4 (&dst)[NK]) {
+        const T* wrow = w + (long long)(a * 32 + l32) * wld + 8 * h;
+#pragma unroll
+        for (int kb = 0; kb < NK; ++kb) dst[kb] = *reinterpret_cast<const uint4*>(wrow + kb * 16);
+    };
+    load_a(0, af[0]);
+    hc_barrier();   // src complete
+    for (int bi = wv; bi < nb; bi += NWV) {
+        const int px = bi * 32 + l32;
+        const int pxc = px < NPX ? px : NPX - 1;
+        uint4 bf[NK];
+#pragma unroll
+        for (int kb = 0; kb < NK; ++kb) bf[kb] = *reinterpret_cast<const uint4*>(src + pxc * ss + 8 * h + kb * 16);
+        if (bi != wv) load_a(0, af[0]);
+#pragma unroll
+        for (int a = 0; a < NA_MAX; ++a) {
+            if (a >= na) break;
+            if (a + 1 < na) load_a(a + 1, af[(a + 1) & 1]);
+            f32x16 acc;
+#pragma unroll
+            for (int e = 0; e < 16; ++e) acc[e] = 0.f;
+#pragma unroll
+            for (int kb = 0; kb < NK; ++kb) acc = HMfma<T>::step(af[a & 1][kb], bf[kb], acc);
+            if (px < NPX) {
+                // register i of lane (l32, h): cout a*32 + (i & 3) + 8 (i >> 2) + 4 h, pixel px
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const int co = a * 32 + 8 * q + 4 * h;
+                    if (co >= M) continue;
+                    const float4 bb = *reinterpret_cast<const float4*>(bias + co);
+                    float v[4] = {acc[4 * q] + bb.x, acc[4 * q + 1] + bb.y, acc[4 * q + 2] + bb.z,
+                                  acc[4 * q + 3] + bb.w};
+                    T o4[4];
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) o4[e] = fromf<T>(silu_act ? silu<T>(v[e]) : v[e]);
+                    store(px, co, *reinterpret_cast<const uint2*>(o4));
+                }
+            }
+        }
+    }
+}
+
+// K (channels) in 16-blocks is a template parameter so the fragment arrays stay in VGPRs;
+// the phase opens with its own barrier (after the first A loads are issued)
+template <typename T, typename Store>
+__device__ __forceinline__ void hc_pw(const T* src, int ss, int NPX, int K, const T* w, int wld, const float* bias,
+                                      int M, bool silu_act, Store store) {
+    switch (K >> 4) {
+        case 4: hc_pw_k<T, 4>(src, ss, NPX, w, wld, bias, M, silu_act, store); break;
+        case 5: hc_pw_k<T, 5>(src, ss, NPX, w, wld, bias, M, silu_act, store); break;
+        case 8: hc_pw_k<T, 8>(src, ss, NPX, w, wld, bias, M, silu_act, store); break;
+        default: __builtin_trap();
+    }
+}
+
+template <typename T>
+__global__ __launch_bounds__(HEAD_CLS_THREADS, 3) void head_cls(const HeadClsArgs A) {
+    extern __shared__ __attribute__((aligned(16))) char hsm[];
+    int li = 0;
+    if (A.nlv > 1 && (int)blockIdx.x >= A.lv[1].wg0) li = 1;
+    if (A.nlv > 2 && (int)blockIdx.x >= A.lv[2].wg0) li = 2;
+    const HeadClsLevel& V = A.lv[li];
+    const int wl = blockIdx.x - V.wg0;
+    const int n = wl / V.tiles, tix = wl - n * V.tiles;
+    const int ty = tix / V.ntw, tx = tix - ty * V.ntw;
+    const int TH = V.TH, TW = V.TW, H = V.H, W = V.W;
+    const int h0 = ty * TH, w0 = tx * TW;
+    const int XH = TH + 4, XW = TW + 4, MH = TH + 2, MW = TW + 2;
+    const int C0 = V.C0, c3 = A.c3;
+    const HcLayout L = hc_layout(TH, TW, C0, c3);
+    T* R1 = reinterpret_cast<T*>(hsm);
+    T* R2 = reinterpret_cast<T*>(hsm + L.r1);
+    const T* x = reinterpret_cast<const T*>(V.x);
+
+    // 1-2. per 64-channel chunk: input tile with a 2-pixel halo (zeros outside the image =
+    //      dw1's zero padding) -> R1, then dw1 of the chunk over the MH x MW mid region -> R2
+    const int ck = C0 < HC_CK ? C0 : HC_CK;
+    for (int cl = 0; cl < C0; cl += ck) {
+        const int cpp = ck >> 3, total = XH * XW * cpp;
+        constexpr int U = 4;
+        for (int q0 = threadIdx.x; q0 < total; q0 += U * HEAD_CLS_THREADS) {
+            uint4 v[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int q = min(q0 + u * HEAD_CLS_THREADS, total - 1);
+                const int px = q / cpp, c = q - px * cpp;
+                const int r = px / XW, cc = px - r * XW;
+                const int gh = h0 - 2 + r, gw = w0 - 2 + cc;
+                const bool ok = (unsigned)gh < (unsigned)H && (unsigned)gw < (unsigned)W;
+                const long long off = ok ? (((long long)n * H + gh) * W + gw) * V.ldx + cl + c * 8 : 0;
+                const uint4 t = *reinterpret_cast<const uint4*>(x + off);
+                v[u] = ok ? t : make_uint4(0, 0, 0, 0);
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int q = q0 + u * HEAD_CLS_THREADS;
+                if (q < total) {
+                    const int px = q / cpp, c = q - px * cpp;
+                    *reinterpret_cast<uint4*>(R1 + px * L.SX + c * 8) = v[u];
+                }
+            }
+        }
+        if (!(A.dbg & 1)) hc_dw<T>(R1, XW, L.SX, R2, MH, MW, L.SD, cl, ck, V.dw1w, V.dw1ld, V.dw1b);
+        else hc_barrier();
+        if (cl + ck < C0) hc_barrier();   // the next chunk overwrites R1
+    }
+    // 3. pw1: D1 (R2) -> P1 (R1), zero outside the image (dw2's zero padding)
+    if (A.dbg & 2) hc_barrier();
+    else
+        hc_pw<T>(R2, L.SD, MH * MW, C0, reinterpret_cast<const T*>(V.pw1w), V.pw1ld, V.pw1b, c3, true,
+                 [&](int px, int co, uint2 v) {
+                     const int r = px / MW, cc = px - r * MW;
+                     const int gh = h0 - 1 + r, gw = w0 - 1 + cc;
+                     if (!((unsigned)gh < (unsigned)H && (unsigned)gw < (unsigned)W)) v = make_uint2(0, 0);
+                     *reinterpret_cast<uint2*>(R1 + px * L.SM + co) = v;
+                 });
+    // 4. dw2 (opens with the barrier after pw1): P1 (R1) -> D2 (R2) over the TH x TW tile
+    if (!(A.dbg & 4)) hc_dw<T>(R1, MW, L.SM, R2, TH, TW, L.SM, 0, c3, V.dw2w, V.dw2ld, V.dw2b);
+    else hc_barrier();
+    // 5. pw2: D2 (R2) -> P2 (R1)
+    if (A.dbg & 8) hc_barrier();
+    else
+        hc_pw<T>(R2, L.SM, TH * TW, c3, reinterpret_cast<const T*>(V.pw2w), V.pw2ld, V.pw2b, c3, true,
+                 [&](int px, int co, uint2 v) { *reinterpret_cast<uint2*>(R1 + px * L.SM + co) = v; });
+    // 6. pw3: P2 (R1) -> class logits in the head tensor
+    T* y = reinterpret_cast<T*>(V.y);
+    if (A.dbg & 16) hc_barrier();
+    else
+        hc_pw<T>(R1, L.SM, TH * TW, c3, reinterpret_cast<const T*>(V.pw3w), V.pw3ld, V.pw3b, A.nc, false,
+                 [&](int px, int co, uint2 v) {
+                     const int r = px / TW, cc = px - r * TW;
+                     const int gh = h0 + r, gw = w0 + cc;
+                     if ((unsigned)gh < (unsigned)H && (unsigned)gw < (unsigned)W)
+                         *reinterpret_cast<uint2*>(y + (((long long)n * H + gh) * W + gw) * V.ldy + co) = v;
+                 });
+}
+
+}  // namespace
+
+int head_cls_lds(int TH, int TW, int C0, int c3, int nc) {
+    if (C0 % 64 && C0 > 64) return 0;            // whole 64-channel chunks
+    // K blocks of the pointwise convs: instantiated 4, 5, 8 (C0 64 / 128, c3 64 / 80 / 128)
+    auto kok = [](int k) { return k == 64 || k == 80 || k == 128; };
+    if ((c3 + 31) / 32 > 4 || (nc + 31) / 32 > 4) return 0;
+    if (!kok(C0) || !kok(c3)) return 0;
+    const HcLayout L = hc_layout(TH, TW, C0, c3);
+    return L.total <= HEAD_CLS_LDS ? L.total : 0;
+}
+
+template <typename T>
+static int launch_head_cls_t(const HeadClsArgs& a, hipStream_t s) {
+    int grid = 0, lds = 0;
+    for (int l = 0; l < a.nlv; ++l) {
+        const HeadClsLevel& v = a.lv[l];
+        const int b = head_cls_lds(v.TH, v.TW, v.C0, a.c3, a.nc);
+        if (b == 0 || v.wg0 != grid) return (int)hipErrorInvalidValue;
+        grid += a.B * v.tiles;
+        lds = lds > b ? lds : b;
+    }
+    hipLaunchKernelGGL((head_cls<T>), dim3((unsigned)grid), dim3(HEAD_CLS_THREADS), lds, s, a);
+    return (int)hipGetLastError();
+}
+
+int launch_head_cls(int dtype, const HeadClsArgs& a, hipStream_t s) {
+    switch (dtype) {
+        case F16: return launch_head_cls_t<_Float16>(a, s);
+        case BF16: return launch_head_cls_t<__bf16>(a, s);
+    }
+    return (int)hipErrorInvalidValue;
+}
+
+}  // namespace yh
