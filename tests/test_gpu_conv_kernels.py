@@ -30,7 +30,7 @@ def test_all_conv_plans_bit_identical(gpu, variant, dtype, batch, size):
     eng.load_module(model)
     x = synth.synth_scenes(batch, size, size, seed=11).to(gpu, dtype)
     outs, names = {}, set()
-    for k in range(8):
+    for k in range(14):
         eng.force_conv_kernel(k)
         outs[k] = eng.forward(x).clone()
         names |= {o["kernel"] for o in eng.ops(batch, size, size) if o["cls"] in ("conv1x1", "conv3x3")}

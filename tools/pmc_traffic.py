@@ -1,5 +1,5 @@
-"""HBM traffic per conv launch from two rocprofv3 --pmc passes (FETCH_SIZE, WRITE_SIZE)
-of tools/pmc_run.py, mapped onto the engine's ops.
+"""HBM traffic per op from two rocprofv3 --pmc passes (FETCH_SIZE, WRITE_SIZE) of
+tools/pmc_run.py, mapped onto the engine's ops.
 
   python tools/pmc_traffic.py <fetch_dir> <write_dir> <ops.json> [out.json]
 
@@ -11,8 +11,9 @@ Corrections per MI355X_MICROARCH.md (HBM / rocprofv3 section):
 Infinity-Cache hits are counted as fabric requests, so this is L2-miss traffic
 (an upper bound on HBM bytes).
 
-The last forward of the workload has exactly one conv-kernel dispatch per
-OP_CONV op, in op order: the last N conv dispatches are matched to the N conv ops.
+The dispatches after the marker (a torch fill kernel) are one eager forward: one
+dispatch per op, except multi-kernel ops (attention: 2) which take the following
+dispatches of their family (tools/trace_ops.py's mapping).
 """
 import csv
 import glob
@@ -21,7 +22,8 @@ import os
 import re
 import sys
 
-CONV_RE = re.compile(r"conv_(direct|gemm2|gemm|stream)(<|I)")
+FAMILY = {"stem": r"conv_first", "dwconv": r"dwconv", "sppf": r"sppf|maxpool",
+          "attention": r"psa_attention|pe_add", "decode": r"head_decode", "head_cls": r"head_cls"}
 
 
 def dispatches(d, counter):
@@ -37,51 +39,61 @@ def dispatches(d, counter):
                 did = int(r["Dispatch_Id"])
                 rec = rows.setdefault(did, dict(name=r["Kernel_Name"], value=0.0))
                 rec["value"] += float(r["Counter_Value"])
-    return [rows[k] for k in sorted(rows)]
+    out = [rows[k] for k in sorted(rows)]
+    mk = max(i for i, r in enumerate(out) if "fill" in r["name"].lower())
+    return [r for r in out[mk + 1:] if "set_io" not in r["name"]]
 
 
-def conv_values(d, counter, n):
-    rows = [r for r in dispatches(d, counter) if CONV_RE.search(r["name"])]
-    if len(rows) < n:
-        raise SystemExit(f"{counter}: {len(rows)} conv dispatches < {n} conv ops")
-    return rows[-n:]
+def per_op(disp, ops):
+    vals, j = [], 0
+    for i, o in enumerate(ops):
+        v = disp[j]["value"]
+        j += 1
+        pat = FAMILY.get(o["cls"])
+        if o["cls"] not in ("conv1x1", "conv3x3"):
+            while pat and j < len(disp) and re.search(pat, disp[j]["name"]) and \
+                    (i + 1 >= len(ops) or ops[i + 1]["cls"] != o["cls"]):
+                v += disp[j]["value"]
+                j += 1
+        vals.append(v)
+    if j != len(disp):
+        raise SystemExit(f"mapped {j} of {len(disp)} dispatches")
+    return vals
 
 
 def main():
-    fetch_dir, write_dir, ops_json = sys.argv[1:4]
-    out = sys.argv[4] if len(sys.argv) > 4 else None
-    ops = json.load(open(ops_json))
-    conv_ops = [o for o in ops if o["cls"] in ("conv3x3", "conv1x1")]
-    n = len(conv_ops)
-    fr = conv_values(fetch_dir, "FETCH_SIZE", n)
-    wr = conv_values(write_dir, "WRITE_SIZE", n)
-    per_op = []
-    for o, f, w in zip(conv_ops, fr, wr):
-        rd = f["value"] * 1024 * 2
-        wb = w["value"] * 1024
-        per_op.append(dict(label=o["label"], cls=o["cls"], kernel=f["name"][:80], alg_bytes=o["bytes"],
-                           read_bytes=rd, write_bytes=wb, traffic=rd + wb, ratio=(rd + wb) / o["bytes"]))
+    fdir, wdir, opsf = sys.argv[1:4]
+    meta = json.load(open(opsf))
+    ops = meta["ops"]
+    fetch = per_op(dispatches(fdir, "FETCH_SIZE"), ops)
+    write = per_op(dispatches(wdir, "WRITE_SIZE"), ops)
     fam = {}
-    for cls in ("conv3x3", "conv1x1"):
-        rows = [r for r in per_op if r["cls"] == cls]
-        if not rows:
-            continue
-        fam[cls] = dict(launches=len(rows),
-                        traffic_per_launch=sum(r["traffic"] for r in rows) / len(rows),
-                        alg_bytes_per_launch=sum(r["alg_bytes"] for r in rows) / len(rows),
-                        traffic_over_alg=sum(r["traffic"] for r in rows) / sum(r["alg_bytes"] for r in rows))
-    cfg = dict(variant=os.environ.get("YH_VARIANT", "n"), size=int(os.environ.get("YH_SIZE", "640")),
-               batch=int(os.environ.get("YH_BATCH", "32")), dtype="bf16")
-    rec = dict(config=cfg, source="rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of tools/pmc_run.py",
-               corrections="KiB x1024; FETCH_SIZE x2 (gfx950 wide-read half count)", family=fam, ops=per_op)
-    for cls, v in fam.items():
-        print(f"{cls}: {v['launches']} launches, traffic {v['traffic_per_launch'] / 1e6:.2f} MB/launch vs "
-              f"algorithmic {v['alg_bytes_per_launch'] / 1e6:.2f} MB ({v['traffic_over_alg']:.2f}x)")
-    for r in sorted(per_op, key=lambda r: -r["traffic"])[:12]:
-        print(f"  {r['label']:28s} {r['traffic'] / 1e6:8.2f} MB  alg {r['alg_bytes'] / 1e6:8.2f} MB  {r['ratio']:.2f}x")
-    if out:
-        with open(out, "w") as f:
-            json.dump(rec, f, indent=1)
+    rows = []
+    for o, fv, wv in zip(ops, fetch, write):
+        t = fv * 1024 * 2 + wv * 1024
+        rows.append(dict(label=o["label"], cls=o["cls"], alg=o["bytes"], traffic=t, ratio=t / max(1.0, o["bytes"])))
+        c = fam.setdefault(o["cls"], dict(launches=0, alg=0.0, traffic=0.0))
+        c["launches"] += 1
+        c["alg"] += o["bytes"]
+        c["traffic"] += t
+    for c in fam.values():
+        c["traffic_per_launch"] = c["traffic"] / c["launches"]
+        c["traffic_over_alg"] = c["traffic"] / c["alg"]
+    tot_alg = sum(c["alg"] for c in fam.values())
+    tot = sum(c["traffic"] for c in fam.values())
+    print(f"forward: algorithmic {tot_alg / 1e6:.1f} MB, PMC traffic {tot / 1e6:.1f} MB ({tot / tot_alg:.2f}x)")
+    for k, c in sorted(fam.items(), key=lambda kv: -kv[1]["traffic"]):
+        print(f"  {k:10s} {c['launches']:3d} launches  alg {c['alg'] / 1e6:8.1f} MB  traffic {c['traffic'] / 1e6:8.1f} MB "
+              f"({c['traffic_over_alg']:.2f}x)")
+    for r in sorted(rows, key=lambda r: -(r["traffic"] - r["alg"]))[:15]:
+        print(f"    {r['label']:34s} {r['cls']:9s} alg {r['alg'] / 1e6:7.1f} MB traffic {r['traffic'] / 1e6:7.1f} MB "
+              f"({r['ratio']:.2f}x)")
+    if len(sys.argv) > 4:
+        with open(sys.argv[4], "w") as f:
+            json.dump(dict(config=meta.get("config"),
+                           source="rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of tools/pmc_run.py (one eager forward)",
+                           corrections="KiB x1024; FETCH_SIZE x2 (gfx950 wide-read half count)",
+                           total=dict(alg=tot_alg, traffic=tot), family=fam, ops=rows), f, indent=1)
 
 
 if __name__ == "__main__":

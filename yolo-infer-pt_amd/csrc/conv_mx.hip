@@ -994,17 +994,19 @@ std::vector<MxPlan> mx_candidates(const MxShape& sh, int num_cus) {
         c.ncb = ncb; c.nbi = nbi; c.nbuf = nbuf;
         cfgs.push_back(c);
     };
+    // 32-pixel wave tiles (mb 1) give small layers (40x40, 20x20) 2-4x more wave tasks
     if (sh.ks == 3 && sh.s == 1) {
-        if (narrow) { addr(1, 2, 1, 4); addr(1, 2, 2, 7); addr(1, 4, 1, 6); }
-        else { addr(2, 2, 1, 4); addr(2, 2, 2, 7); }
+        if (narrow) { addr(1, 2, 1, 4); addr(1, 2, 2, 7); addr(1, 4, 1, 6); addr(1, 1, 1, 2); addr(1, 1, 2, 4); }
+        else { addr(2, 2, 1, 4); addr(2, 2, 2, 7); addr(2, 1, 1, 2); addr(2, 1, 2, 4); }
     } else if (sh.ks == 3) {
         // stride 2: a 4x8 wave tile (9x17 patch) double-buffered, or an 8x8 tile (17x17)
         // single-buffered; 32-cout slices for weights too large to keep whole
         if (narrow) { addr(1, 1, 1, 5); addr(1, 2, 1, 10, 1); }
         else { addr(2, 1, 1, 5); addr(2, 2, 1, 10, 1); addr(1, 1, 1, 5); addr(1, 2, 1, 10, 1); }
     } else {
-        if (narrow) { addr(1, 2, 1, 2); addr(1, 2, 2, 4); addr(1, 2, 4, 8); addr(1, 4, 1, 4); addr(1, 4, 2, 8); }
-        else { addr(2, 2, 1, 2); addr(2, 2, 2, 4); addr(2, 2, 4, 8); }
+        if (narrow) { addr(1, 2, 1, 2); addr(1, 2, 2, 4); addr(1, 2, 4, 8); addr(1, 4, 1, 4); addr(1, 4, 2, 8);
+                      addr(1, 1, 2, 2); addr(1, 1, 4, 4); }
+        else { addr(2, 2, 1, 2); addr(2, 2, 2, 4); addr(2, 2, 4, 8); addr(2, 1, 2, 2); addr(2, 1, 4, 4); }
     }
     std::vector<MxPlan> out;
     for (auto& c : cfgs) {
@@ -1175,6 +1177,14 @@ int launch_mxr_cfg(const MxPlan& pl, const MxArgs& a, hipStream_t s) {
     YH_MXR(3, 2, 1, 2, 1, 10, 1)
     YH_MXR(3, 2, 2, 1, 1, 5, 2)
     YH_MXR(3, 2, 1, 1, 1, 5, 2)
+    YH_MXR(3, 1, 2, 1, 1, 2, 2)
+    YH_MXR(3, 1, 2, 1, 2, 4, 2)
+    YH_MXR(3, 1, 1, 1, 1, 2, 2)
+    YH_MXR(3, 1, 1, 1, 2, 4, 2)
+    YH_MXR(1, 1, 2, 1, 2, 2, 2)
+    YH_MXR(1, 1, 2, 1, 4, 4, 2)
+    YH_MXR(1, 1, 1, 1, 2, 2, 2)
+    YH_MXR(1, 1, 1, 1, 4, 4, 2)
     YH_MXR(1, 1, 2, 2, 1, 2, 2)
     YH_MXR(1, 1, 2, 2, 2, 4, 2)
     YH_MXR(1, 1, 2, 2, 4, 8, 2)

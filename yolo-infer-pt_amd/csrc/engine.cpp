@@ -791,6 +791,18 @@ struct Net {
             conv_args(ops[i], B, H, W, a, BM, BN);
             cands[i] = mx_candidates(mx_shape(a, B), num_cus);
             require(!cands[i].empty(), "no conv_mx plan for " + ops[i].label);
+            // YH_MX_LDS_MAX=<bytes> (experiments): only plans within an LDS budget, leaving
+            // CU room for other streams' kernels (forward lanes); the smallest plan if none fits
+            static const int lds_max = [] { const char* e = getenv("YH_MX_LDS_MAX"); return e ? atoi(e) : 0; }();
+            if (lds_max > 0) {
+                std::vector<MxPlan> keep;
+                for (auto& pl : cands[i])
+                    if (pl.lds <= lds_max) keep.push_back(pl);
+                if (keep.empty())
+                    keep.push_back(*std::min_element(cands[i].begin(), cands[i].end(),
+                                                     [](const MxPlan& x, const MxPlan& y) { return x.lds < y.lds; }));
+                cands[i] = keep;
+            }
             const int pick = forced >= 0 ? std::min(forced, (int)cands[i].size() - 1) : 0;
             ch[i].plan = cands[i][pick];
             ch[i].name = mx_name(ch[i].plan);
