@@ -254,6 +254,8 @@ def main():
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
+    # marker dispatch for traces (tools/trace_stats.py): the timed steps follow it
+    torch.zeros(1, device=dev).fill_(7.0)
     if dist:
         torch.distributed.barrier()
     torch.cuda.synchronize()
@@ -265,6 +267,7 @@ def main():
         torch.distributed.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
+    torch.zeros(1, device=dev).fill_(8.0)   # end marker (outside the timed region)
     if dist:
         t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
