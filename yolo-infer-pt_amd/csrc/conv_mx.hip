@@ -988,9 +988,9 @@ std::vector<MxPlan> mx_candidates(const MxShape& sh, int num_cus) {
         }
     }
     // resident-weight per-wave kernels (instantiated set, see launch_mxr_cfg)
-    auto addr = [&](int na, int mb, int ncb, int nbi, int nbuf = 2) {
+    auto addr = [&](int na, int mb, int ncb, int nbi, int nbuf = 2, int nw = 8) {
         MxConfig c{};
-        c.kind = 1; c.ks = sh.ks; c.s = sh.ks == 1 ? 1 : sh.s; c.na = na; c.mb = mb; c.wn = 1; c.wm = 8;
+        c.kind = 1; c.ks = sh.ks; c.s = sh.ks == 1 ? 1 : sh.s; c.na = na; c.mb = mb; c.wn = 1; c.wm = nw;
         c.ncb = ncb; c.nbi = nbi; c.nbuf = nbuf;
         cfgs.push_back(c);
     };
@@ -1002,7 +1002,8 @@ std::vector<MxPlan> mx_candidates(const MxShape& sh, int num_cus) {
         // stride 2: a 4x8 wave tile (9x17 patch) double-buffered, or an 8x8 tile (17x17)
         // single-buffered; 32-cout slices for weights too large to keep whole
         if (narrow) { addr(1, 1, 1, 5); addr(1, 2, 1, 10, 1); }
-        else { addr(2, 1, 1, 5); addr(2, 2, 1, 10, 1); addr(1, 1, 1, 5); addr(1, 2, 1, 10, 1); }
+        else { addr(2, 1, 1, 5); addr(2, 2, 1, 10, 1); addr(1, 1, 1, 5); addr(1, 2, 1, 10, 1);
+               addr(2, 1, 2, 10, 2, 4); addr(1, 1, 2, 10, 2, 4); }
     } else {
         if (narrow) { addr(1, 2, 1, 2); addr(1, 2, 2, 4); addr(1, 2, 4, 8); addr(1, 4, 1, 4); addr(1, 4, 2, 8);
                       addr(1, 1, 2, 2); addr(1, 1, 4, 4); }
@@ -1148,26 +1149,30 @@ int launch_mx_cfg(const MxPlan& pl, const MxArgs& a, hipStream_t s) {
     return (int)hipErrorInvalidValue;
 }
 
-template <typename T, int KS, int S, int NA, int MB, int NCB, int NBI, int NBUF>
+template <typename T, int KS, int S, int NA, int MB, int NCB, int NBI, int NBUF, int NW>
 int launch_mxr_t(const MxPlan& pl, const MxArgs& a, hipStream_t s) {
     static bool attr = false;
-    auto k = &conv_mxr<T, KS, S, NA, MB, NCB, NBI, 8, NBUF>;
+    auto k = &conv_mxr<T, KS, S, NA, MB, NCB, NBI, NW, NBUF>;
     if (!attr) {
         (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize,
                                   160 * 1024);
         attr = true;
     }
-    hipLaunchKernelGGL(k, dim3(pl.grid), dim3(512), pl.lds, s, a);
+    hipLaunchKernelGGL(k, dim3(pl.grid), dim3(64 * NW), pl.lds, s, a);
     return (int)hipGetLastError();
 }
 
 template <typename T>
 int launch_mxr_cfg(const MxPlan& pl, const MxArgs& a, hipStream_t s) {
     const MxConfig& c = pl.cfg;
-#define YH_MXR(KS_, S_, NA_, MB_, NCB_, NBI_, NBUF_)                                                  \
+#define YH_MXRW(KS_, S_, NA_, MB_, NCB_, NBI_, NBUF_, NW_)                                            \
     if (c.ks == KS_ && c.s == S_ && c.na == NA_ && c.mb == MB_ && c.ncb == NCB_ && c.nbi == NBI_ &&      \
-        c.nbuf == NBUF_)                                                                                \
-        return launch_mxr_t<T, KS_, S_, NA_, MB_, NCB_, NBI_, NBUF_>(pl, a, s);
+        c.nbuf == NBUF_ && c.wm == NW_)                                                                 \
+        return launch_mxr_t<T, KS_, S_, NA_, MB_, NCB_, NBI_, NBUF_, NW_>(pl, a, s);
+#define YH_MXR(KS_, S_, NA_, MB_, NCB_, NBI_, NBUF_) YH_MXRW(KS_, S_, NA_, MB_, NCB_, NBI_, NBUF_, 8)
+    // stride 2, 32-channel stages with 4 waves: each stage reads 64 of a pixel's 128 B
+    YH_MXRW(3, 2, 2, 1, 2, 10, 2, 4)
+    YH_MXRW(3, 2, 1, 1, 2, 10, 2, 4)
     YH_MXR(3, 1, 2, 2, 1, 4, 2)
     YH_MXR(3, 1, 2, 2, 2, 7, 2)
     YH_MXR(3, 1, 1, 2, 1, 4, 2)
@@ -1194,6 +1199,7 @@ int launch_mxr_cfg(const MxPlan& pl, const MxArgs& a, hipStream_t s) {
     YH_MXR(1, 1, 1, 4, 1, 4, 2)
     YH_MXR(1, 1, 1, 4, 2, 8, 2)
 #undef YH_MXR
+#undef YH_MXRW
     return (int)hipErrorInvalidValue;
 }
 
