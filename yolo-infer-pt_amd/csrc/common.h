@@ -122,9 +122,11 @@ struct HeadClsArgs {
     HeadClsLevel lv[3];
     int nlv, B, c3, nc;
     int dbg;                         // experiments (YH_HCLS_DBG): bit k skips phase k (0 dw1 .. 4 pw3)
+    unsigned long long* trace;       // experiments (YH_HCLS_TRACE): [grid][8] s_memrealtime stamps
+    const void* zero;                // >= 16 zero bytes (source of out-of-image / padding chunks)
 };
 constexpr int HEAD_CLS_THREADS = 256;
-constexpr int HEAD_CLS_LDS = 40 * 1024;    // four workgroups (16 waves) per CU
+constexpr int HEAD_CLS_LDS = 80 * 1024;    // two workgroups (8 waves) per CU: 8x16 tiles at 80x80
 // LDS bytes of a tile's buffers; 0 if it does not fit
 int head_cls_lds(int TH, int TW, int C0, int c3, int nc);
 int launch_head_cls(int dtype, const HeadClsArgs& a, hipStream_t s);

@@ -439,7 +439,7 @@ struct Net {
     // output tile of one level of the fused cls branch: the largest candidate whose
     // workgroup (resident weights + one tile's buffers) fits the LDS
     static bool head_cls_tile(int C0, int c3, int nc, int H, int W, int& TH, int& TW) {
-        static const int cand[][2] = {{8, 16}, {8, 8}, {4, 16}, {4, 8}, {8, 4}, {4, 4}, {2, 8}, {2, 4}, {2, 2}};
+        static const int cand[][2] = {{16, 16}, {8, 32}, {8, 16}, {8, 8}, {4, 16}, {4, 8}, {8, 4}, {4, 4}, {2, 8}, {2, 4}, {2, 2}};
         for (auto& c : cand) {
             if (c[0] > H || c[1] > W) continue;
             if (head_cls_lds(c[0], c[1], C0, c3, nc) > 0) {
@@ -882,6 +882,7 @@ struct Net {
             total += cost[k];
         }
         if (const char* e = getenv("YH_HCLS_DBG")) a.dbg = atoi(e);
+        a.zero = zero_dev;
         // one workgroup per tile, the 80x80 level (most work) first
         int wg = 0;
         for (int k = 0; k < nl; ++k) {
@@ -927,7 +928,47 @@ struct Net {
             case OP_DW: rc = launch_dwconv(dtype, dw_args(op, B, H, W), s); break;
             case OP_SPPF: rc = launch_sppf(dtype, pool_args(op, B, H, W), s); break;
             case OP_ATTN: rc = launch_attention(dtype, attn_args(op, H, W), B, s); break;
-            case OP_HEADCLS: rc = launch_head_cls(dtype, head_cls_args(op, B, H, W), s); break;
+            case OP_HEADCLS: {
+                HeadClsArgs a = head_cls_args(op, B, H, W);
+                // YH_HCLS_TRACE=1 (experiments, eager launches only): per-workgroup phase stamps
+                static const bool trace = getenv("YH_HCLS_TRACE") != nullptr;
+                hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+                (void)hipStreamIsCapturing(s, &cs);
+                static unsigned long long* tbuf = nullptr;
+                int grid = 0;
+                for (int l = 0; l < a.nlv; ++l) grid += B * a.lv[l].tiles;
+                if (trace && cs == hipStreamCaptureStatusNone) {
+                    static int cap = 0;
+                    if (grid > cap) {
+                        if (tbuf) (void)hipFree(tbuf);
+                        HIPCHECK(hipMalloc(&tbuf, (size_t)grid * 64));
+                        cap = grid;
+                    }
+                    a.trace = tbuf;
+                }
+                rc = launch_head_cls(dtype, a, s);
+                if (rc == 0 && a.trace) {
+                    HIPCHECK(hipStreamSynchronize(s));
+                    std::vector<unsigned long long> h((size_t)grid * 8);
+                    HIPCHECK(hipMemcpy(h.data(), tbuf, h.size() * 8, hipMemcpyDeviceToHost));
+                    unsigned long long t0 = ~0ull, t1 = 0;
+                    std::vector<double> ph[6];
+                    for (int g = 0; g < grid; ++g) {
+                        const unsigned long long* r = &h[(size_t)g * 8];
+                        t0 = std::min(t0, r[0]);
+                        t1 = std::max(t1, r[6]);
+                        for (int k = 0; k < 6; ++k) ph[k].push_back((r[k + 1] - r[k]) * 0.01);
+                    }
+                    fprintf(stderr, "[head_cls] span %.1f us, per-WG phase medians (us):", (t1 - t0) * 0.01);
+                    static const char* nm[6] = {"load", "dw1", "pw1", "dw2", "pw2", "pw3"};
+                    for (int k = 0; k < 6; ++k) {
+                        std::sort(ph[k].begin(), ph[k].end());
+                        fprintf(stderr, " %s %.2f", nm[k], ph[k][ph[k].size() / 2]);
+                    }
+                    fprintf(stderr, "\n");
+                }
+                break;
+            }
             case OP_DECODE: {
                 DecodeArgs a{};
                 for (int l = 0; l < 3; ++l) {

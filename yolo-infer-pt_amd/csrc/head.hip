@@ -12,6 +12,8 @@
 // conv_mx's K order (16-channel blocks ascending, one v_mfma_f32_32x32x16 step each, fp32
 // accumulator, + bias, activation, one rounding). The first pointwise output is zeroed
 // outside the image: it is the second depthwise conv's zero padding.
+#include <cstdlib>
+
 #include "common.h"
 #include "dtypes.h"
 
@@ -37,6 +39,18 @@ template <> struct HMfma<_Float16> {
 
 constexpr int NWV = HEAD_CLS_THREADS / 64;
 
+// LDS-DMA: the wave's 64 lanes each copy 16 B from their own global address into LDS at
+// lds_addr + 16 * lane (M0 holds the wave-uniform base; restored after the copy)
+__device__ __forceinline__ void hc_glds(const void* src, unsigned lds_addr) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    unsigned keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep) : "v"(src), "s"(lds_addr) : "memory");
+#else
+    (void)src; (void)lds_addr;
+#endif
+}
+
 // Workgroup barrier for LDS hand-offs only: __syncthreads() also waits for every global
 // load in flight (vmcnt(0)), which would drain the weight loads issued ahead of a phase.
 __device__ __forceinline__ void hc_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
@@ -46,19 +60,22 @@ constexpr int HC_RB = 4;     // output rows per depthwise item (register sliding
 // LDS of one tile: region 1 = the input chunk (XH x XW x min(C0, HC_CK)), later the first /
 // second pointwise outputs; region 2 = the first / second depthwise outputs
 struct HcLayout {
-    int SX, SD, SM, r1, total;
+    int SX, SD, SM, r1, prm, total;   // prm: byte offset of the fp32 parameters (see hc_params)
 };
 __host__ __device__ inline HcLayout hc_layout(int TH, int TW, int C0, int c3) {
     HcLayout L;
     const int ck = C0 < HC_CK ? C0 : HC_CK;
     L.SX = ck + 8; L.SD = C0 + 8; L.SM = c3 + 8;
     const int MP = (TH + 2) * (TW + 2), NO = TH * TW;
-    const int x = (TH + 4) * (TW + 4) * L.SX * 2, p1 = MP * L.SM * 2, p2 = NO * L.SM * 2;
+    const int x = ((TH + 4) * (TW + 4) * L.SX * 2 + 1023) & ~1023;   // whole LDS-DMA instructions
+    const int p1 = MP * L.SM * 2, p2 = NO * L.SM * 2;
     const int d1 = MP * L.SD * 2, d2 = NO * L.SM * 2;
     int a = x > p1 ? x : p1;
     a = a > p2 ? a : p2;
     L.r1 = (a + 15) & ~15;
-    L.total = L.r1 + (d1 > d2 ? d1 : d2);
+    L.prm = L.r1 + (((d1 > d2 ? d1 : d2) + 15) & ~15);
+    // dw1 weights [9][C0] + bias, dw2 weights [9][c3] + bias, pw1 / pw2 / pw3 bias (HC_NA * 32 each)
+    L.total = L.prm + (((10 * C0 + 10 * c3 + 3 * 96) * 4 + 1023) & ~1023);
     return L;
 }
 
@@ -80,8 +97,8 @@ __device__ __forceinline__ void hc_dw(const T* src, int SW, int ss, T* dst, int 
         bb = *reinterpret_cast<const float4*>(b + c0);
         wg = g;
     };
+    hc_barrier();   // src (and the parameters in LDS) complete
     if ((int)threadIdx.x < ng * per_g) load_w(threadIdx.x / per_g);
-    hc_barrier();   // src complete
     for (int q = threadIdx.x; q < ng * per_g; q += HEAD_CLS_THREADS) {
         const int g = q / per_g, rem = q - g * per_g;
         const int rb = rem / DW, c = rem - rb * DW;
@@ -122,24 +139,32 @@ __device__ __forceinline__ void hc_dw(const T* src, int SW, int ss, T* dst, int 
 
 // Pointwise conv phase: A = weights [rows][wld] (dtype, global; rows >= na * 32 zero-padded)
 // times the NPX pixels of LDS `src` (stride ss, 16 NK channels). The A fragments of the first
-// 32-cout tile are loaded before the barrier that opens the phase (they do not depend on
-// LDS), the next tile's while the current one's MFMAs run. Each wave takes 32-pixel B tiles
-// round-robin (B fragments read once per B tile). K order: 16-channel blocks ascending.
-// store(px, co, 4 rounded values) for couts co < M.
-template <typename T, int NK, typename Store>
-__device__ __forceinline__ void hc_pw_k(const T* src, int ss, int NPX, const T* w, int wld, const float* bias, int M,
-                                        bool silu_act, Store store) {
-    constexpr int NA_MAX = 4;
+// NAP 32-cout tiles are loaded ahead of the phase (hc_pw_pre, one phase earlier: their
+// latency hides behind the previous phase); tiles past NAP are loaded in the loop, one tile
+// ahead. Each wave takes 32-pixel B tiles round-robin (B fragments read once per B tile).
+// K order: 16-channel blocks ascending. store(px, co, 4 rounded values) for couts co < M.
+constexpr int HC_NA = 3;   // 32-cout tiles per pointwise conv (cout <= 96)
+template <int NK, int NAP>
+struct HcA {
+    uint4 f[NAP][NK];
+};
+template <typename T, int NK, int NAP>
+__device__ __forceinline__ void hc_pw_pre(const T* w, int wld, int M, HcA<NK, NAP>& A) {
+    const int lane = threadIdx.x & 63, l32 = lane & 31, h = lane >> 5;
+    const int na = (M + 31) >> 5;
+#pragma unroll
+    for (int a = 0; a < NAP; ++a) {
+        const T* wrow = w + (long long)(min(a, na - 1) * 32 + l32) * wld + 8 * h;
+#pragma unroll
+        for (int kb = 0; kb < NK; ++kb) A.f[a][kb] = *reinterpret_cast<const uint4*>(wrow + kb * 16);
+    }
+}
+template <typename T, int NK, int NAP, typename Store>
+__device__ __forceinline__ void hc_pw_run(const T* src, int ss, int NPX, const T* w, int wld, const float* bias, int M,
+                                          bool silu_act, const HcA<NK, NAP>& A, Store store) {
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const int l32 = lane & 31, h = lane >> 5;
     const int na = (M + 31) >> 5, nb = (NPX + 31) >> 5;
-    uint4 af[2][NK];   // A fragments of couts tiles a (af[a & 1]) and a + 1
-    auto load_a = [&](int a, uint4 (&dst)[NK]) {
-        const T* wrow = w + (long long)(a * 32 + l32) * wld + 8 * h;
-#pragma unroll
-        for (int kb = 0; kb < NK; ++kb) dst[kb] = *reinterpret_cast<const uint4*>(wrow + kb * 16);
-    };
-    load_a(0, af[0]);
     hc_barrier();   // src complete
     for (int bi = wv; bi < nb; bi += NWV) {
         const int px = bi * 32 + l32;
@@ -147,16 +172,27 @@ __device__ __forceinline__ void hc_pw_k(const T* src, int ss, int NPX, const T* 
         uint4 bf[NK];
 #pragma unroll
         for (int kb = 0; kb < NK; ++kb) bf[kb] = *reinterpret_cast<const uint4*>(src + pxc * ss + 8 * h + kb * 16);
-        if (bi != wv) load_a(0, af[0]);
+        uint4 lf[2][NK];   // tiles past NAP: double-buffered loads
+        auto load_a = [&](int a, uint4 (&dst)[NK]) {
+            const T* wrow = w + (long long)(a * 32 + l32) * wld + 8 * h;
 #pragma unroll
-        for (int a = 0; a < NA_MAX; ++a) {
+            for (int kb = 0; kb < NK; ++kb) dst[kb] = *reinterpret_cast<const uint4*>(wrow + kb * 16);
+        };
+        if (NAP < na) load_a(NAP, lf[NAP & 1]);
+#pragma unroll
+        for (int a = 0; a < HC_NA; ++a) {
             if (a >= na) break;
-            if (a + 1 < na) load_a(a + 1, af[(a + 1) & 1]);
+            if (a >= NAP && a + 1 < na) load_a(a + 1, lf[(a + 1) & 1]);
             f32x16 acc;
 #pragma unroll
             for (int e = 0; e < 16; ++e) acc[e] = 0.f;
+            if (a < NAP) {
 #pragma unroll
-            for (int kb = 0; kb < NK; ++kb) acc = HMfma<T>::step(af[a & 1][kb], bf[kb], acc);
+                for (int kb = 0; kb < NK; ++kb) acc = HMfma<T>::step(A.f[a < NAP ? a : 0][kb], bf[kb], acc);
+            } else {
+#pragma unroll
+                for (int kb = 0; kb < NK; ++kb) acc = HMfma<T>::step(lf[a & 1][kb], bf[kb], acc);
+            }
             if (px < NPX) {
                 // register i of lane (l32, h): cout a*32 + (i & 3) + 8 (i >> 2) + 4 h, pixel px
 #pragma unroll
@@ -176,25 +212,15 @@ __device__ __forceinline__ void hc_pw_k(const T* src, int ss, int NPX, const T* 
     }
 }
 
-// K (channels) in 16-blocks is a template parameter so the fragment arrays stay in VGPRs;
-// the phase opens with its own barrier (after the first A loads are issued)
-template <typename T, typename Store>
-__device__ __forceinline__ void hc_pw(const T* src, int ss, int NPX, int K, const T* w, int wld, const float* bias,
-                                      int M, bool silu_act, Store store) {
-    switch (K >> 4) {
-        case 4: hc_pw_k<T, 4>(src, ss, NPX, w, wld, bias, M, silu_act, store); break;
-        case 5: hc_pw_k<T, 5>(src, ss, NPX, w, wld, bias, M, silu_act, store); break;
-        case 8: hc_pw_k<T, 8>(src, ss, NPX, w, wld, bias, M, silu_act, store); break;
-        default: __builtin_trap();
-    }
-}
-
-template <typename T>
-__global__ __launch_bounds__(HEAD_CLS_THREADS, 3) void head_cls(const HeadClsArgs A) {
-    extern __shared__ __attribute__((aligned(16))) char hsm[];
-    int li = 0;
-    if (A.nlv > 1 && (int)blockIdx.x >= A.lv[1].wg0) li = 1;
-    if (A.nlv > 2 && (int)blockIdx.x >= A.lv[2].wg0) li = 2;
+// One workgroup = one output tile of level li. NK1 = C0 / 16 and NK2 = c3 / 16 (K blocks of
+// the first and the later pointwise convs); NAP1 = pw1 A tiles loaded ahead (all three when
+// the registers allow).
+template <typename T, int NK1, int NAP1, int NK2>
+__device__ __forceinline__ void hc_body(const HeadClsArgs& A, int li, char* hsm) {
+    unsigned long long st[8];
+    const bool tr = A.trace != nullptr;
+    auto stamp = [&](int i) { if (tr) st[i] = __builtin_amdgcn_s_memrealtime(); };
+    stamp(0);
     const HeadClsLevel& V = A.lv[li];
     const int wl = blockIdx.x - V.wg0;
     const int n = wl / V.tiles, tix = wl - n * V.tiles;
@@ -206,81 +232,135 @@ __global__ __launch_bounds__(HEAD_CLS_THREADS, 3) void head_cls(const HeadClsArg
     const HcLayout L = hc_layout(TH, TW, C0, c3);
     T* R1 = reinterpret_cast<T*>(hsm);
     T* R2 = reinterpret_cast<T*>(hsm + L.r1);
+    // depthwise weights and every bias in LDS (read in the phases' inner loops / epilogues)
+    float* PW1 = reinterpret_cast<float*>(hsm + L.prm);
+    float* PB1 = PW1 + 9 * C0;
+    float* PW2 = PB1 + C0;
+    float* PB2 = PW2 + 9 * c3;
+    float* QB1 = PB2 + c3;
+    float* QB2 = QB1 + 96;
+    float* QB3 = QB2 + 96;
+    // the parameters are contiguous fp32 arrays (ld == channels): one flat list of 16-B
+    // chunks, loaded into registers before the input tile's loads, stored after them
+    // parameters by LDS-DMA (no registers held): segment starts in 16-B chunks
+    const int e0 = 9 * C0 / 4, e1 = e0 + C0 / 4, e2 = e1 + 9 * c3 / 4, e3 = e2 + c3 / 4;
+    const int e4 = e3 + 24, e5 = e4 + 24, e6 = e5 + 24;
+    typedef __attribute__((address_space(3))) char* lds_c;
+    const unsigned lds0 = (unsigned)(size_t)(lds_c)hsm;
+    {
+        const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+        for (int i0 = wv * 64; i0 < e6; i0 += HEAD_CLS_THREADS) {
+            const int q = i0 + lane;
+            const float* src = q < e0 ? V.dw1w + 4 * q
+                             : q < e1 ? V.dw1b + 4 * (q - e0)
+                             : q < e2 ? V.dw2w + 4 * (q - e1)
+                             : q < e3 ? V.dw2b + 4 * (q - e2)
+                             : q < e4 ? V.pw1b + 4 * (q - e3)
+                             : q < e5 ? V.pw2b + 4 * (q - e4)
+                             : q < e6 ? V.pw3b + 4 * (q - e5) : reinterpret_cast<const float*>(A.zero);
+            hc_glds(src, lds0 + (unsigned)L.prm + (unsigned)i0 * 16);
+        }
+    }
     const T* x = reinterpret_cast<const T*>(V.x);
+    HcA<NK1, NAP1> A1;   // pw1's weights, in flight while the input tile loads
+    hc_pw_pre<T, NK1, NAP1>(reinterpret_cast<const T*>(V.pw1w), V.pw1ld, c3, A1);
 
     // 1-2. per 64-channel chunk: input tile with a 2-pixel halo (zeros outside the image =
     //      dw1's zero padding) -> R1, then dw1 of the chunk over the MH x MW mid region -> R2
     const int ck = C0 < HC_CK ? C0 : HC_CK;
     for (int cl = 0; cl < C0; cl += ck) {
-        const int cpp = ck >> 3, total = XH * XW * cpp;
-        constexpr int U = 4;
-        for (int q0 = threadIdx.x; q0 < total; q0 += U * HEAD_CLS_THREADS) {
-            uint4 v[U];
-#pragma unroll
-            for (int u = 0; u < U; ++u) {
-                const int q = min(q0 + u * HEAD_CLS_THREADS, total - 1);
-                const int px = q / cpp, c = q - px * cpp;
+        // the padded tile (SX = ck + 8: cpp data chunks + 1 pad chunk per pixel) by LDS-DMA,
+        // zeros outside the image = dw1's zero padding
+        const int cpp = ck >> 3, cpx = cpp + 1, total = XH * XW * cpx;
+        {
+            const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+            for (int i0 = wv * 64; i0 < total; i0 += HEAD_CLS_THREADS) {
+                const int q = i0 + lane;
+                const int px = q / cpx, c = q - px * cpx;
                 const int r = px / XW, cc = px - r * XW;
                 const int gh = h0 - 2 + r, gw = w0 - 2 + cc;
-                const bool ok = (unsigned)gh < (unsigned)H && (unsigned)gw < (unsigned)W;
-                const long long off = ok ? (((long long)n * H + gh) * W + gw) * V.ldx + cl + c * 8 : 0;
-                const uint4 t = *reinterpret_cast<const uint4*>(x + off);
-                v[u] = ok ? t : make_uint4(0, 0, 0, 0);
-            }
-#pragma unroll
-            for (int u = 0; u < U; ++u) {
-                const int q = q0 + u * HEAD_CLS_THREADS;
-                if (q < total) {
-                    const int px = q / cpp, c = q - px * cpp;
-                    *reinterpret_cast<uint4*>(R1 + px * L.SX + c * 8) = v[u];
-                }
+                const bool ok = q < total && c < cpp && (unsigned)gh < (unsigned)H && (unsigned)gw < (unsigned)W;
+                const void* src = ok ? (const void*)(x + (((long long)n * H + gh) * W + gw) * V.ldx + cl + c * 8) : A.zero;
+                hc_glds(src, lds0 + (unsigned)i0 * 16);
             }
         }
-        if (!(A.dbg & 1)) hc_dw<T>(R1, XW, L.SX, R2, MH, MW, L.SD, cl, ck, V.dw1w, V.dw1ld, V.dw1b);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's DMAs (and earlier loads) landed
+        stamp(1);
+        if (!(A.dbg & 1)) hc_dw<T>(R1, XW, L.SX, R2, MH, MW, L.SD, cl, ck, PW1, C0, PB1);
         else hc_barrier();
+        stamp(2);
         if (cl + ck < C0) hc_barrier();   // the next chunk overwrites R1
     }
     // 3. pw1: D1 (R2) -> P1 (R1), zero outside the image (dw2's zero padding)
     if (A.dbg & 2) hc_barrier();
     else
-        hc_pw<T>(R2, L.SD, MH * MW, C0, reinterpret_cast<const T*>(V.pw1w), V.pw1ld, V.pw1b, c3, true,
-                 [&](int px, int co, uint2 v) {
-                     const int r = px / MW, cc = px - r * MW;
-                     const int gh = h0 - 1 + r, gw = w0 - 1 + cc;
-                     if (!((unsigned)gh < (unsigned)H && (unsigned)gw < (unsigned)W)) v = make_uint2(0, 0);
-                     *reinterpret_cast<uint2*>(R1 + px * L.SM + co) = v;
-                 });
+        hc_pw_run<T, NK1, NAP1>(R2, L.SD, MH * MW, reinterpret_cast<const T*>(V.pw1w), V.pw1ld, QB1, c3, true, A1,
+                                [&](int px, int co, uint2 v) {
+                                    const int r = px / MW, cc = px - r * MW;
+                                    const int gh = h0 - 1 + r, gw = w0 - 1 + cc;
+                                    if (!((unsigned)gh < (unsigned)H && (unsigned)gw < (unsigned)W))
+                                        v = make_uint2(0, 0);
+                                    *reinterpret_cast<uint2*>(R1 + px * L.SM + co) = v;
+                                });
+    HcA<NK2, HC_NA> A2;   // pw2's weights, in flight during dw2
+    hc_pw_pre<T, NK2, HC_NA>(reinterpret_cast<const T*>(V.pw2w), V.pw2ld, c3, A2);
+    stamp(3);
     // 4. dw2 (opens with the barrier after pw1): P1 (R1) -> D2 (R2) over the TH x TW tile
-    if (!(A.dbg & 4)) hc_dw<T>(R1, MW, L.SM, R2, TH, TW, L.SM, 0, c3, V.dw2w, V.dw2ld, V.dw2b);
+    if (!(A.dbg & 4)) hc_dw<T>(R1, MW, L.SM, R2, TH, TW, L.SM, 0, c3, PW2, c3, PB2);
     else hc_barrier();
+    stamp(4);
     // 5. pw2: D2 (R2) -> P2 (R1)
     if (A.dbg & 8) hc_barrier();
     else
-        hc_pw<T>(R2, L.SM, TH * TW, c3, reinterpret_cast<const T*>(V.pw2w), V.pw2ld, V.pw2b, c3, true,
-                 [&](int px, int co, uint2 v) { *reinterpret_cast<uint2*>(R1 + px * L.SM + co) = v; });
+        hc_pw_run<T, NK2, HC_NA>(R2, L.SM, TH * TW, reinterpret_cast<const T*>(V.pw2w), V.pw2ld, QB2, c3, true, A2,
+                                 [&](int px, int co, uint2 v) { *reinterpret_cast<uint2*>(R1 + px * L.SM + co) = v; });
+    HcA<NK2, HC_NA> A3;   // pw3's weights: issued once pw2's are dead
+    hc_pw_pre<T, NK2, HC_NA>(reinterpret_cast<const T*>(V.pw3w), V.pw3ld, A.nc, A3);
+    stamp(5);
     // 6. pw3: P2 (R1) -> class logits in the head tensor
     T* y = reinterpret_cast<T*>(V.y);
     if (A.dbg & 16) hc_barrier();
     else
-        hc_pw<T>(R1, L.SM, TH * TW, c3, reinterpret_cast<const T*>(V.pw3w), V.pw3ld, V.pw3b, A.nc, false,
-                 [&](int px, int co, uint2 v) {
-                     const int r = px / TW, cc = px - r * TW;
-                     const int gh = h0 + r, gw = w0 + cc;
-                     if ((unsigned)gh < (unsigned)H && (unsigned)gw < (unsigned)W)
-                         *reinterpret_cast<uint2*>(y + (((long long)n * H + gh) * W + gw) * V.ldy + co) = v;
-                 });
+        hc_pw_run<T, NK2, HC_NA>(R1, L.SM, TH * TW, reinterpret_cast<const T*>(V.pw3w), V.pw3ld, QB3, A.nc, false,
+                                 A3, [&](int px, int co, uint2 v) {
+                                     const int r = px / TW, cc = px - r * TW;
+                                     const int gh = h0 + r, gw = w0 + cc;
+                                     if ((unsigned)gh < (unsigned)H && (unsigned)gw < (unsigned)W)
+                                         *reinterpret_cast<uint2*>(y + (((long long)n * H + gh) * W + gw) * V.ldy + co) = v;
+                                 });
+    stamp(6);
+    if (tr && threadIdx.x == 0) {
+        unsigned long long* o = A.trace + (size_t)blockIdx.x * 8;
+        for (int k = 0; k < 7; ++k) o[k] = st[k];
+        o[7] = (unsigned long long)li;
+    }
+}
+
+template <typename T>
+__global__ __launch_bounds__(HEAD_CLS_THREADS, 3) void head_cls(const HeadClsArgs A) {
+    extern __shared__ __attribute__((aligned(16))) char hsm[];
+    int li = 0;
+    if (A.nlv > 1 && (int)blockIdx.x >= A.lv[1].wg0) li = 1;
+    if (A.nlv > 2 && (int)blockIdx.x >= A.lv[2].wg0) li = 2;
+    const int nk1 = A.lv[li].C0 >> 4, nk2 = A.c3 >> 4;
+    if (nk1 == 4 && nk2 == 5) hc_body<T, 4, HC_NA, 5>(A, li, hsm);
+    else if (nk1 == 8 && nk2 == 5) hc_body<T, 8, 1, 5>(A, li, hsm);
+    else if (nk1 == 4 && nk2 == 4) hc_body<T, 4, HC_NA, 4>(A, li, hsm);
+    else if (nk1 == 8 && nk2 == 4) hc_body<T, 8, 1, 4>(A, li, hsm);
 }
 
 }  // namespace
 
 int head_cls_lds(int TH, int TW, int C0, int c3, int nc) {
     if (C0 % 64 && C0 > 64) return 0;            // whole 64-channel chunks
-    // K blocks of the pointwise convs: instantiated 4, 5, 8 (C0 64 / 128, c3 64 / 80 / 128)
-    auto kok = [](int k) { return k == 64 || k == 80 || k == 128; };
-    if ((c3 + 31) / 32 > 4 || (nc + 31) / 32 > 4) return 0;
-    if (!kok(C0) || !kok(c3)) return 0;
+    // instantiated: C0 64 / 128, c3 64 / 80, at most three 32-cout tiles per pointwise conv
+    if (!(C0 == 64 || C0 == 128) || !(c3 == 64 || c3 == 80) || nc > 32 * HC_NA) return 0;
+    // parameter chunks: 10 (C0 + c3) / 4 + 72 <= 4 per thread
+    if ((10 * (C0 + c3)) / 4 + 72 > 4 * HEAD_CLS_THREADS) return 0;
     const HcLayout L = hc_layout(TH, TW, C0, c3);
-    return L.total <= HEAD_CLS_LDS ? L.total : 0;
+    // YH_HCLS_LDS=<bytes> (experiments): tile LDS budget (default HEAD_CLS_LDS)
+    static const int budget = [] { const char* e = getenv("YH_HCLS_LDS"); return e ? atoi(e) : HEAD_CLS_LDS; }();
+    return L.total <= budget && L.total <= 160 * 1024 ? L.total : 0;
 }
 
 template <typename T>
@@ -292,6 +372,12 @@ static int launch_head_cls_t(const HeadClsArgs& a, hipStream_t s) {
         if (b == 0 || v.wg0 != grid) return (int)hipErrorInvalidValue;
         grid += a.B * v.tiles;
         lds = lds > b ? lds : b;
+    }
+    static bool attr = false;
+    if (!attr) {
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&head_cls<T>),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        attr = true;
     }
     hipLaunchKernelGGL((head_cls<T>), dim3((unsigned)grid), dim3(HEAD_CLS_THREADS), lds, s, a);
     return (int)hipGetLastError();
