@@ -190,7 +190,8 @@ int yh_op_count(const yh_handle* h);
 
 /* Describe op `index` for an input of (batch, height, width): label (module
  * path), class (0 dense 3x3 conv, 1 dense 1x1 conv, 2 stem conv, 3 depthwise,
- * 4 SPPF pools, 5 PSA attention, 6 head decode), algorithmic bytes (each
+ * 4 SPPF pools, 5 PSA attention, 6 head decode, 7 fused head cls branch,
+ * 8 fused box tail with DFL), algorithmic bytes (each
  * operand read once, each output written once, handle dtype) and FLOPs per
  * call, accumulated profiled milliseconds and call count. */
 int yh_op_info(const yh_handle* h, int index, int batch, int height, int width,
@@ -200,18 +201,17 @@ int yh_op_info(const yh_handle* h, int index, int batch, int height, int width,
 /* Use a captured HIP graph for yh_forward (default on). */
 int yh_set_graph(yh_handle* h, int enable);
 
-/* Kernel that runs op `index` at (batch, height, width): for dense convs the
- * implementation the per-shape tuner picked on the first yh_forward at that
- * shape ("gemm", "gemm64", "gemm128", "stream", "direct", "stream4",
- * "stream8", "tiny"; all bit-identical; a layer may instead run "ksplit4",
- * chosen by a fixed shape rule), for the other ops the op's single kernel name.
- * YH_ESTATE before that forward. */
+/* Kernel that runs op `index` at (batch, height, width): for a dense conv of a
+ * 16-bit handle the conv_mx plan the per-shape tuner picked on the first
+ * yh_forward at that shape (e.g. "mxr_k3s1_na2_mb2_b1x2_nb2"; every plan is
+ * bit-identical), "gemm_f32" on the fp32 handle, for the other ops the op's
+ * kernel name. YH_ESTATE before that forward. */
 int yh_op_kernel(const yh_handle* h, int index, int batch, int height, int width, const char** name);
 
-/* Force dense-conv kernel `kernel` (0..7, the order of the names above) on every
- * conv that supports it (the others run "gemm"), or -1 to return to per-shape
- * autotuning. Drops the tuned choices and captured graphs. Testing hook: every
- * kernel must produce bit-identical outputs. */
+/* Force conv plan `kernel` (an index into each conv's candidate list, clamped)
+ * on every dense conv, or -1 to return to per-shape autotuning. Drops the tuned
+ * choices and captured graphs. Testing hook: every plan must produce
+ * bit-identical outputs. */
 int yh_force_conv_kernel(yh_handle* h, int kernel);
 
 /* Launch units of the forward at (batch, height, width), known after the first

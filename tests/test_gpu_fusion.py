@@ -4,7 +4,9 @@ Marked gpu.
 The fused op recomputes the same layers in the same arithmetic order (per-channel depthwise
 FMA chains, conv_mx's K order on v_mfma_f32_32x32x16, one rounding per layer output), so the
 head output must be exactly equal with fusion on (default) and off (YH_FUSE=0 at handle
-creation), for every shape: whole and partial tiles, every level, both 16-bit dtypes.
+creation), for every shape: whole and partial tiles, every level, both 16-bit dtypes. The same holds
+for the folded decode (box_dfl writes the box rows, head_cls or a class-rows decode the
+scores), including anchor counts that are not a multiple of 8 (96 x 160: A = 315).
 """
 import os
 
@@ -33,7 +35,8 @@ def _engine(model, dtype, dev, fuse):
 
 
 @pytest.mark.parametrize("variant,dtype,batch,h,w", [("n", torch.bfloat16, 4, 640, 640), ("n", torch.float16, 2, 320, 256),
-                                                     ("s", torch.bfloat16, 2, 384, 640), ("x", torch.bfloat16, 1, 320, 320)])
+                                                     ("s", torch.bfloat16, 2, 384, 640), ("x", torch.bfloat16, 1, 320, 320),
+                                                     ("n", torch.float16, 3, 96, 160)])
 def test_fused_head_equals_per_layer_launches(gpu, variant, dtype, batch, h, w):
     model = make_model(variant)
     x = synth.synth_scenes(batch, h, w, seed=31).to(gpu, dtype)
@@ -41,7 +44,8 @@ def test_fused_head_equals_per_layer_launches(gpu, variant, dtype, batch, h, w):
     plain = _engine(model, dtype, gpu, False)
     kinds_f = {o["cls"] for o in fused.ops(batch, h, w)}
     kinds_p = {o["cls"] for o in plain.ops(batch, h, w)}
-    assert "head_cls" not in kinds_p
+    assert "head_cls" not in kinds_p and "box_dfl" not in kinds_p
+    assert "box_dfl" in kinds_f   # decode folded into the box tail (+ head_cls / class-rows decode)
     if variant == "n":   # s (128) / x (384) cls branches keep the per-layer launches
         assert "head_cls" in kinds_f
         assert len(fused.ops(batch, h, w)) < len(plain.ops(batch, h, w))

@@ -79,6 +79,8 @@ struct DecodeArgs {
     const void* lvl[3]; int ldc; int H[3], W[3]; float stride[3];
     int nc, A, B;
     const void* const* io;  // io[1] = y (B, 4+nc, A)
+    int a_lo;               // first anchor decoded (anchors [a_lo, A))
+    int box;                // 0: class rows only (the box rows come from box_dfl)
 };
 
 // NMS (utils/util.py:123-169)
@@ -110,6 +112,7 @@ struct HeadClsLevel {
     const void* x; int ldx, C0;      // level input (NHWC view), channels
     int H, W;
     void* y; int ldy;                // output view (the head tensor's cls slice)
+    int aoff;                        // direct mode: the level's first anchor
     const float* dw1w; const float* dw1b; int dw1ld;   // [9][dw1ld] fp32, bias
     const void* pw1w; int pw1ld; const float* pw1b;    // [rows][pw1ld] dtype, bias
     const float* dw2w; const float* dw2b; int dw2ld;
@@ -124,12 +127,33 @@ struct HeadClsArgs {
     int dbg;                         // experiments (YH_HCLS_DBG): bit k skips phase k (0 dw1 .. 4 pw3)
     unsigned long long* trace;       // experiments (YH_HCLS_TRACE): [grid][8] s_memrealtime stamps
     const void* zero;                // >= 16 zero bytes (source of out-of-image / padding chunks)
+    // direct mode (io != nullptr): pw3's logits leave as sigmoid scores in rows 4.. of the
+    // caller's y = io[1] (B, 4+nc, A) instead of the head tensor (the decode's class part)
+    const void* const* io; int A;
 };
 constexpr int HEAD_CLS_THREADS = 256;
 constexpr int HEAD_CLS_LDS = 80 * 1024;    // two workgroups (8 waves) per CU: 8x16 tiles at 80x80
 // LDS bytes of a tile's buffers; 0 if it does not fit
 int head_cls_lds(int TH, int TW, int C0, int c3, int nc);
 int launch_head_cls(int dtype, const HeadClsArgs& a, hipStream_t s);
+
+// Box tail of the detect head, one launch for all levels: the last box conv (Conv2d 1x1
+// + bias, nets/nn.py:241) with DFL (nn.py:222-225), make_anchors (utils/util.py:85-96) and
+// dist2bbox (nn.py:264-268) in its epilogue, writing rows 0..3 of y = io[1]. Bit-identical
+// to the conv launch + head_decode (same MFMA K order, logits rounded to the dtype first).
+struct BoxDflLevel {
+    const void* x; int ldx;          // box.l.1 output (NHWC), K = 16 * nk channels
+    int H, W; float stride; int aoff;
+    const void* w; int wld; const float* b;   // [64][wld] dtype weights, fp32 bias
+    int wg0;                         // first workgroup of the level
+};
+struct BoxDflArgs {
+    BoxDflLevel lv[3];
+    int nlv, B, nk, nc, A;
+    const void* const* io;
+};
+constexpr int BOX_DFL_TPW = 4;       // 32-pixel tiles per wave (4 waves per workgroup)
+int launch_box_dfl(int dtype, const BoxDflArgs& a, hipStream_t s);
 
 // launchers (return hipError_t as int)
 bool conv_kernel_ok(int dtype, int kern, const ConvArgs& a);

@@ -89,9 +89,9 @@ static uint16_t f2h(float f) {
 
 // ---------------------------------------------------------------- graph model
 enum ConvKind { CK_DENSE = 0, CK_FIRST = 1, CK_DW = 2, CK_PE = 3 };
-enum OpKind { OP_FIRST, OP_CONV, OP_DW, OP_SPPF, OP_ATTN, OP_DECODE, OP_HEADCLS };
+enum OpKind { OP_FIRST, OP_CONV, OP_DW, OP_SPPF, OP_ATTN, OP_DECODE, OP_HEADCLS, OP_BOXDFL };
 enum OpClass { CL_CONV3 = 0, CL_CONV1 = 1, CL_FIRST = 2, CL_DW = 3, CL_SPPF = 4, CL_ATTN = 5, CL_DECODE = 6,
-               CL_HEADCLS = 7, CL_N = 8 };
+               CL_HEADCLS = 7, CL_BOXDFL = 8, CL_N = 9 };
 
 struct Tensor { int level; int C; };        // physical channels = pixel stride
 struct View { int t = -1; int coff = 0; int C = 0; };
@@ -126,6 +126,13 @@ struct Op {
     int hc[3][5] = {};
     View hx[3], hy[3];
     bool hlv[3] = {false, false, false};   // levels the fused op covers
+    bool direct = false;                   // OP_HEADCLS: scores straight into y (decode folded in)
+    // OP_BOXDFL: per level the last box conv and its input (the box.l.1 output)
+    int bc[3] = {-1, -1, -1};
+    View bx[3];
+    // OP_DECODE: first level decoded, and whether the box rows are (false: box_dfl writes them)
+    int dlo = 0;
+    bool dbox = true;
     std::string label;
 };
 
@@ -376,25 +383,40 @@ struct Net {
         // per level, coarsest first: the 20x20 and 40x40 head branches join the
         // level program that computes P5 / P4; the 80x80 level runs last
         for (int l = 0; l < 3; ++l) L[l] = tensor(3 + l, 64 + ncp);
-        // 16-bit handles run the three cls branches as one fused launch (head.hip) when
-        // every level has an LDS tile; YH_FUSE=0 keeps the per-layer launches
+        // 16-bit handles run the cls branches of the levels that have an LDS tile as one
+        // fused launch (head.hip), and fold the decode into the producers of the logits: the
+        // box rows into box_dfl (last box conv + DFL), the fused levels' scores into
+        // head_cls, the other levels' (a suffix) into a class-rows decode. YH_FUSE=0 keeps
+        // the per-layer launches and the decode.
+        bool fl[3];
+        for (int l = 0; l < 3; ++l) fl[l] = fuse_head_cls(xc[l], clsc, nc);
+        const bool fdec = fuse_decode(boxc, nc) && (fl[0] || !fl[1]) && (fl[1] || !fl[2]);
         bool fuse_any = false;
         Op hcop;
         hcop.kind = OP_HEADCLS;
         hcop.label = "head.cls";
+        hcop.direct = fdec;
+        Op bdop;
+        bdop.kind = OP_BOXDFL;
+        bdop.label = "head.box_dfl";
         for (int l : {2, 1, 0}) {
             const int lvl = 3 + l;
             const std::string bp = "head.box." + std::to_string(l);
             const int tb1 = tensor(lvl, boxc), tb2 = tensor(lvl, boxc);
             conv3(bp + ".0", full(xs[l], xc[l]), xc[l], boxc, 1, ACT_SILU, full(tb1, boxc));
             conv3(bp + ".1", full(tb1, boxc), boxc, boxc, 1, ACT_SILU, full(tb2, boxc));
-            dense(bp + ".2", {Seg{full(tb2, boxc), 0}}, {boxc}, 64, 1, 1, ACT_ID, slice(L[l], 0, 64), nullptr, 1);
+            if (fdec) {
+                bdop.bc[l] = new_dense_conv(bp + ".2", boxc, 64, 1, 1, ACT_ID);
+                bdop.bx[l] = full(tb2, boxc);
+            } else {
+                dense(bp + ".2", {Seg{full(tb2, boxc), 0}}, {boxc}, 64, 1, 1, ACT_ID, slice(L[l], 0, 64), nullptr, 1);
+            }
             const std::string cp = "head.cls." + std::to_string(l);
             View o;
             o.t = L[l];
             o.coff = 64;
             o.C = ncp;
-            if (fuse_head_cls(xc[l], clsc, nc)) {
+            if (fl[l]) {
                 // the same five convs (weights are loaded by name), no per-layer ops
                 fuse_any = hcop.hlv[l] = true;
                 hcop.hc[l][0] = new_conv(cp + ".0", CK_DW, xc[l], xc[l], 3, 1, xc[l], 0, ACT_SILU);
@@ -414,11 +436,17 @@ struct Net {
             dense(cp + ".4", {Seg{full(tc4, clsc), 0}}, {clsc}, nc, 1, 1, ACT_ID, o, nullptr, 1);
         }
         if (fuse_any) ops.push_back(hcop);
+        if (fdec) ops.push_back(bdop);
         Op dec;
         dec.kind = OP_DECODE;
         for (int l = 0; l < 3; ++l) dec.lvl[l] = full(L[l]);
         dec.label = "head.decode";
-        ops.push_back(dec);
+        dec.dbox = !fdec;
+        dec.dlo = fdec ? (fl[2] ? 3 : fl[1] ? 2 : fl[0] ? 1 : 0) : 0;
+        if (dec.dlo < 3) {
+            if (fdec) dec.label = "head.decode_cls";
+            ops.push_back(dec);
+        }
         finalize_convs();
     }
     // a dense conv with a single unsegmented input and no op of its own (fused ops)
@@ -426,6 +454,19 @@ struct Net {
         const int ci = new_conv(name, CK_DENSE, cin, cout, k, 1, 1, has_bias, act);
         convs[ci].segs.push_back({cin, round_up(cin, 8)});
         return ci;
+    }
+    // the decode folds into box_dfl + head_cls / a class-rows decode (16-bit handles; the
+    // box branch's last conv has 4 or 6 16-channel K blocks)
+    bool fuse_decode(int boxc, int nc) const {
+        const char* e = getenv("YH_FUSE");
+        if (dtype == F32 || (e && atoi(e) == 0)) return false;
+        return (boxc == 64 || boxc == 96) && nc % 4 == 0;
+    }
+    // first anchor of detect level l (0..2) for an H x W input (make_anchors order)
+    static int anchor_off(int l, int H, int W) {
+        int a = 0;
+        for (int k = 0; k < l; ++k) a += (H >> (3 + k)) * (W >> (3 + k));
+        return a;
     }
     // a level's cls branch is fused when it has 16-channel blocks, 4-channel class groups
     // and an LDS tile next to its resident weights
@@ -845,9 +886,9 @@ struct Net {
         HeadClsArgs a{};
         a.B = B;
         a.nc = var.num_classes;
-        a.c3 = convs[op.hc[0][1]].cout;
-        // one persistent workgroup per CU, split over the levels by estimated work
-        double cost[3], total = 0;
+        int l0 = 0;
+        while (!op.hlv[l0]) ++l0;
+        a.c3 = convs[op.hc[l0][1]].cout;
         int lvls[3], nl = 0;
         for (int l = 0; l < 3; ++l)
             if (op.hlv[l]) lvls[nl++] = l;
@@ -862,6 +903,7 @@ struct Net {
             v.C0 = op.hx[l].C;
             v.y = ptr(op.hy[l]);
             v.ldy = ldc(op.hy[l]);
+            v.aoff = anchor_off(l, H, W);
             const ConvDesc &d1 = convs[op.hc[l][0]], &p1 = convs[op.hc[l][1]], &d2 = convs[op.hc[l][2]],
                            &p2 = convs[op.hc[l][3]], &p3 = convs[op.hc[l][4]];
             require(d1.loaded && p1.loaded && d2.loaded && p2.loaded && p3.loaded, "head.cls weights not loaded");
@@ -873,23 +915,49 @@ struct Net {
             require(head_cls_tile(v.C0, a.c3, a.nc, v.H, v.W, v.TH, v.TW), "head.cls: no LDS tile");
             v.ntw = (v.W + v.TW - 1) / v.TW;
             v.tiles = v.ntw * ((v.H + v.TH - 1) / v.TH);
-            const double mp = (v.TH + 2.0) * (v.TW + 2.0), no = (double)v.TH * v.TW;
-            const double c3p = 32.0 * ((a.c3 + 31) / 32), ncp = 32.0 * ((a.nc + 31) / 32);
-            // MACs per tile (depthwise VALU weighted 4x an MFMA MAC) + the input tile's bytes
-            cost[k] = (double)B * v.tiles *
-                      (mp * v.C0 * (36.0 + c3p) + no * a.c3 * (36.0 + c3p + ncp) +
-                       64.0 * (v.TH + 4.0) * (v.TW + 4.0) * v.C0);
-            total += cost[k];
         }
         if (const char* e = getenv("YH_HCLS_DBG")) a.dbg = atoi(e);
         a.zero = zero_dev;
+        if (op.direct) {
+            a.io = (const void* const*)io_dev;
+            a.A = anchor_off(3, H, W);
+        }
         // one workgroup per tile, the 80x80 level (most work) first
         int wg = 0;
         for (int k = 0; k < nl; ++k) {
             a.lv[k].wg0 = wg;
             wg += B * a.lv[k].tiles;
         }
-        (void)cost; (void)total;
+        return a;
+    }
+
+    BoxDflArgs box_dfl_args(const Op& op, int B, int H, int W) {
+        BoxDflArgs a{};
+        a.B = B;
+        a.nc = var.num_classes;
+        a.A = anchor_off(3, H, W);
+        a.io = (const void* const*)io_dev;
+        a.nk = op.bx[0].C / 16;
+        int wg = 0;
+        for (int l = 0; l < 3; ++l) {
+            BoxDflLevel& v = a.lv[a.nlv++];
+            const ConvDesc& d = convs[op.bc[l]];
+            require(d.loaded, "head.box weights not loaded");
+            require(d.cin == 16 * a.nk && d.cout == 64 && d.cout_p >= 64, "box_dfl: conv shape");
+            const int lv = tensors[op.bx[l].t].level;
+            v.x = ptr(op.bx[l]);
+            v.ldx = ldc(op.bx[l]);
+            v.H = H >> lv;
+            v.W = W >> lv;
+            v.stride = (float)(1 << lv);
+            v.aoff = anchor_off(l, H, W);
+            v.w = d.w_dev;
+            v.wld = d.Kp;
+            v.b = d.b_dev;
+            v.wg0 = wg;
+            const long long tiles = ((long long)B * v.H * v.W + 31) / 32;
+            wg += (int)((tiles + 4 * BOX_DFL_TPW - 1) / (4 * BOX_DFL_TPW));
+        }
         return a;
     }
 
@@ -982,9 +1050,12 @@ struct Net {
                 a.A = a.H[0] * a.W[0] + a.H[1] * a.W[1] + a.H[2] * a.W[2];
                 a.B = B;
                 a.io = (const void* const*)io_dev;
+                a.a_lo = anchor_off(op.dlo, H, W);
+                a.box = op.dbox ? 1 : 0;
                 rc = launch_decode(dtype, a, s);
                 break;
             }
+            case OP_BOXDFL: rc = launch_box_dfl(dtype, box_dfl_args(op, B, H, W), s); break;
         }
         if (rc != 0) throw Fail(YH_EHIP, "launch of " + op.label + " failed: " + hipGetErrorString((hipError_t)rc));
     }
@@ -1111,6 +1182,7 @@ struct Net {
             case OP_ATTN: return CL_ATTN;
             case OP_DECODE: return CL_DECODE;
             case OP_HEADCLS: return CL_HEADCLS;
+            case OP_BOXDFL: return CL_BOXDFL;
         }
         return CL_CONV1;
     }
@@ -1178,9 +1250,26 @@ struct Net {
                     A += px(tensors[op.lvl[l].t].level);
                     cin = tensors[op.lvl[l].t].C;
                 }
-                bytes = A * (64 + var.num_classes) * es + A * (4 + var.num_classes) * es;
                 (void)cin;
-                flops = A * (64 * 4.0 + var.num_classes * 4.0);
+                if (op.dbox) {
+                    bytes = A * (64 + var.num_classes) * es + A * (4 + var.num_classes) * es;
+                    flops = A * (64 * 4.0 + var.num_classes * 4.0);
+                } else {
+                    A = 0;
+                    for (int l = op.dlo; l < 3; ++l) A += px(tensors[op.lvl[l].t].level);
+                    bytes = 2.0 * A * var.num_classes * es;
+                    flops = A * var.num_classes * 4.0;
+                }
+                break;
+            }
+            case OP_BOXDFL: {
+                // the box.l.1 outputs read once, 4 box rows written, weights once per level
+                for (int l = 0; l < 3; ++l) {
+                    const double n = px(tensors[op.bx[l].t].level);
+                    const int K = op.bx[l].C;
+                    bytes += n * K * es + n * 4 * es + 64.0 * K * es + 64 * 4.0;
+                    flops += 2.0 * n * 64 * K + n * 64 * 4.0;
+                }
                 break;
             }
         }
@@ -1466,7 +1555,7 @@ int yh_op_kernel(const yh_handle* h, int index, int batch, int height, int width
     return guarded([&] {
         yh::require(h && index >= 0 && index < (int)h->net.ops.size(), "op index out of range");
         const yh::Net& n = h->net;
-        static const char* op_names[] = {"stem", "conv", "dwconv", "sppf", "attention", "decode", "head_cls"};
+        static const char* op_names[] = {"stem", "conv", "dwconv", "sppf", "attention", "decode", "head_cls", "box_dfl"};
         const yh::Op& op = n.ops[index];
         if (op.kind != yh::OP_CONV) {
             if (name) *name = op_names[(int)op.kind];

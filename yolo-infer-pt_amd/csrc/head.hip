@@ -5,7 +5,10 @@
 //              TH x TW output tile of one image of one level; the input tile with a 2-pixel
 //              halo, the first depthwise output and first pointwise output with a 1-pixel
 //              halo, the second depthwise and pointwise outputs all stay in LDS; only the
-//              level input is read from HBM and only the nc class logits are written.
+//              level input is read from HBM and only the nc class logits are written
+//              (direct mode: their sigmoid scores, straight into the caller's y).
+//   box_dfl    the box branch's last 1x1 conv with DFL + anchors + dist2bbox in its
+//              epilogue (rows 0..3 of y); with head_cls's direct mode it replaces the decode.
 //
 // Bit-identical to the unfused launches: the depthwise convs run dwconv3x3_c4's per-channel
 // FMA chain (taps row-major, fp32, + bias, SiLU, one rounding), the pointwise convs run
@@ -38,6 +41,10 @@ template <> struct HMfma<_Float16> {
 };
 
 constexpr int NWV = HEAD_CLS_THREADS / 64;
+
+// the decode's 16-bit exp and division (misc.hip ex<T> / dv<T>): same instructions, same bits
+__device__ __forceinline__ float hx_exp(float x) { return __expf(x); }
+__device__ __forceinline__ float hx_div(float a, float b) { return a * __builtin_amdgcn_rcpf(b); }
 
 // LDS-DMA: the wave's 64 lanes each copy 16 B from their own global address into LDS at
 // lds_addr + 16 * lane (M0 holds the wave-uniform base; restored after the copy)
@@ -317,9 +324,24 @@ __device__ __forceinline__ void hc_body(const HeadClsArgs& A, int li, char* hsm)
     HcA<NK2, HC_NA> A3;   // pw3's weights: issued once pw2's are dead
     hc_pw_pre<T, NK2, HC_NA>(reinterpret_cast<const T*>(V.pw3w), V.pw3ld, A.nc, A3);
     stamp(5);
-    // 6. pw3: P2 (R1) -> class logits in the head tensor
+    // 6. pw3: P2 (R1) -> class logits in the head tensor, or (direct mode) their sigmoid in
+    //    the caller's y, one row per class (the decode's class part: logit rounded first)
     T* y = reinterpret_cast<T*>(V.y);
     if (A.dbg & 16) hc_barrier();
+    else if (A.io)
+        hc_pw_run<T, NK2, HC_NA>(R1, L.SM, TH * TW, reinterpret_cast<const T*>(V.pw3w), V.pw3ld, QB3, A.nc, false,
+                                 A3, [&](int px, int co, uint2 v) {
+                                     const int r = px / TW, cc = px - r * TW;
+                                     const int gh = h0 + r, gw = w0 + cc;
+                                     if ((unsigned)gh < (unsigned)H && (unsigned)gw < (unsigned)W) {
+                                         T* col = reinterpret_cast<T*>(const_cast<void*>(A.io[1])) +
+                                                  ((long long)n * (4 + A.nc) + 4 + co) * A.A + V.aoff + gh * W + gw;
+                                         const T* o = reinterpret_cast<const T*>(&v);
+#pragma unroll
+                                         for (int e = 0; e < 4; ++e)
+                                             col[(long long)e * A.A] = fromf<T>(hx_div(1.0f, 1.0f + hx_exp(-tof(o[e]))));
+                                     }
+                                 });
     else
         hc_pw_run<T, NK2, HC_NA>(R1, L.SM, TH * TW, reinterpret_cast<const T*>(V.pw3w), V.pw3ld, QB3, A.nc, false,
                                  A3, [&](int px, int co, uint2 v) {
@@ -349,7 +371,126 @@ __global__ __launch_bounds__(HEAD_CLS_THREADS, 3) void head_cls(const HeadClsArg
     else if (nk1 == 8 && nk2 == 4) hc_body<T, 8, 1, 4>(A, li, hsm);
 }
 
+// Box tail: each wave takes BOX_DFL_TPW consecutive 32-pixel tiles of a level's flattened
+// (image, row, column) pixels. The 64-cout 1x1 conv runs as two 32x32 MFMA tiles whose rows
+// are permuted so that lane half h holds couts 32h .. 32h+31, i.e. the 16 bins of sides 2h and
+// 2h+1 of its pixel: the DFL softmax / expectation is lane-local, one swap across the halves
+// completes the four distances, and half h writes rows 2h, 2h+1 (32 consecutive anchors per
+// row and store instruction).
+template <typename T, int NK>
+__device__ __forceinline__ void bd_body(const BoxDflArgs& A, int li) {
+    const BoxDflLevel& V = A.lv[li];
+    const int lane = threadIdx.x & 63, l32 = lane & 31, h = lane >> 5, wv = threadIdx.x >> 6;
+    const int HW = V.H * V.W;
+    const long long M = (long long)A.B * HW;
+    const long long tile0 = ((long long)(blockIdx.x - V.wg0) * 4 + wv) * BOX_DFL_TPW;
+    if (tile0 * 32 >= M) return;
+    const T* w = reinterpret_cast<const T*>(V.w);
+    uint4 af[2][NK];
+#pragma unroll
+    for (int a = 0; a < 2; ++a) {
+        const int co = 32 * ((l32 >> 2) & 1) + 16 * a + (l32 & 3) + 4 * (l32 >> 3);
+#pragma unroll
+        for (int kb = 0; kb < NK; ++kb)
+            af[a][kb] = *reinterpret_cast<const uint4*>(w + (long long)co * V.wld + 8 * h + kb * 16);
+    }
+    const T* x = reinterpret_cast<const T*>(V.x);
+    auto load_b = [&](long long t, uint4 (&bf)[NK]) {
+        long long m = t * 32 + l32;
+        m = m < M ? m : M - 1;
+#pragma unroll
+        for (int kb = 0; kb < NK; ++kb) bf[kb] = *reinterpret_cast<const uint4*>(x + m * V.ldx + 8 * h + kb * 16);
+    };
+    float bs[2][16];   // bias of the lane's 32 couts
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int i = 0; i < 16; i += 4) {
+            const float4 q = *reinterpret_cast<const float4*>(V.b + 32 * h + 16 * a + i);
+            bs[a][i] = q.x; bs[a][i + 1] = q.y; bs[a][i + 2] = q.z; bs[a][i + 3] = q.w;
+        }
+    uint4 bf[BOX_DFL_TPW][NK];   // every tile's loads in flight at once (HBM latency)
+#pragma unroll
+    for (int t = 0; t < BOX_DFL_TPW; ++t) load_b(tile0 + t, bf[t]);
+    T* yb = reinterpret_cast<T*>(const_cast<void*>(A.io[1]));
+#pragma unroll
+    for (int t = 0; t < BOX_DFL_TPW; ++t) {
+        const long long tt = tile0 + t;
+        if (tt * 32 >= M) break;
+        float dist[2];
+#pragma unroll
+        for (int a = 0; a < 2; ++a) {
+            f32x16 acc;
+#pragma unroll
+            for (int e = 0; e < 16; ++e) acc[e] = 0.f;
+#pragma unroll
+            for (int kb = 0; kb < NK; ++kb) acc = HMfma<T>::step(af[a][kb], bf[t][kb], acc);
+            // register i: cout 32h + 16a + i = bin i of side 2h + a; the conv's rounding first
+            float v[16];
+#pragma unroll
+            for (int i = 0; i < 16; ++i) v[i] = tof(fromf<T>(acc[i] + bs[a][i]));
+            float mx = v[0];
+#pragma unroll
+            for (int i = 1; i < 16; ++i) mx = fmaxf(mx, v[i]);
+            float sum = 0.f;
+#pragma unroll
+            for (int i = 0; i < 16; ++i) { v[i] = hx_exp(v[i] - mx); sum += v[i]; }
+            float d = 0.f;
+#pragma unroll
+            for (int i = 0; i < 16; ++i) d = fmaf((float)i, hx_div(v[i], sum), d);
+            dist[a] = d;
+        }
+        const float o0 = __shfl_xor(dist[0], 32), o1 = __shfl_xor(dist[1], 32);
+        const float dl = h ? o0 : dist[0], dt = h ? o1 : dist[1];
+        const float dr = h ? dist[0] : o0, db = h ? dist[1] : o1;
+        const long long m = tt * 32 + l32;
+        if (m < M) {
+            const int n = (int)(m / HW), loc = (int)(m - (long long)n * HW);
+            const int gy = loc / V.W, gx = loc - gy * V.W;
+            const float ax = (float)gx + 0.5f, ay = (float)gy + 0.5f, st = V.stride;
+            const float x1 = ax - dl, y1 = ay - dt;
+            const float x2 = ax + dr, y2 = ay + db;
+            const float r0 = h ? (x2 - x1) * st : (x1 + x2) / 2.0f * st;
+            const float r1 = h ? (y2 - y1) * st : (y1 + y2) / 2.0f * st;
+            T* col = yb + ((long long)n * (4 + A.nc) + 2 * h) * A.A + V.aoff + loc;
+            col[0] = fromf<T>(r0);
+            col[A.A] = fromf<T>(r1);
+        }
+    }
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void box_dfl(const BoxDflArgs A) {
+    int li = 0;
+    if (A.nlv > 1 && (int)blockIdx.x >= A.lv[1].wg0) li = 1;
+    if (A.nlv > 2 && (int)blockIdx.x >= A.lv[2].wg0) li = 2;
+    if (A.nk == 4) bd_body<T, 4>(A, li);
+    else if (A.nk == 6) bd_body<T, 6>(A, li);
+}
+
 }  // namespace
+
+template <typename T>
+static int launch_box_dfl_t(const BoxDflArgs& a, hipStream_t s) {
+    if (!(a.nk == 4 || a.nk == 6)) return (int)hipErrorInvalidValue;
+    int grid = 0;
+    for (int l = 0; l < a.nlv; ++l) {
+        const BoxDflLevel& v = a.lv[l];
+        if (v.wg0 != grid || v.ldx % 8 || v.wld % 8) return (int)hipErrorInvalidValue;
+        const long long tiles = ((long long)a.B * v.H * v.W + 31) / 32;
+        grid += (int)((tiles + 4 * BOX_DFL_TPW - 1) / (4 * BOX_DFL_TPW));
+    }
+    hipLaunchKernelGGL((box_dfl<T>), dim3((unsigned)grid), dim3(256), 0, s, a);
+    return (int)hipGetLastError();
+}
+
+int launch_box_dfl(int dtype, const BoxDflArgs& a, hipStream_t s) {
+    switch (dtype) {
+        case F16: return launch_box_dfl_t<_Float16>(a, s);
+        case BF16: return launch_box_dfl_t<__bf16>(a, s);
+    }
+    return (int)hipErrorInvalidValue;
+}
 
 int head_cls_lds(int TH, int TW, int C0, int c3, int nc) {
     if (C0 % 64 && C0 > 64) return 0;            // whole 64-channel chunks

@@ -407,7 +407,7 @@ template <typename T, bool ROWS>
 __global__ __launch_bounds__(256) void head_decode(const DecodeArgs p) {
     extern __shared__ __attribute__((aligned(16))) char dsm[];
     T* tile = reinterpret_cast<T*>(dsm);              // [(4 + nc)][256]
-    const int n = blockIdx.y, a0 = blockIdx.x * 256;
+    const int n = blockIdx.y, a0 = p.a_lo + blockIdx.x * 256;
     const int a = a0 + threadIdx.x;
     const bool live = a < p.A;
     T* yimg = reinterpret_cast<T*>(const_cast<void*>(p.io[1])) + (long long)n * (4 + p.nc) * p.A;
@@ -450,10 +450,12 @@ __global__ __launch_bounds__(256) void head_decode(const DecodeArgs p) {
         const float ax = (float)gx + 0.5f, ay = (float)gy + 0.5f, st = p.stride[l];
         const float x1 = ax - dist[0], y1 = ay - dist[1];
         const float x2 = ax + dist[2], y2 = ay + dist[3];
-        put(0, (x1 + x2) / 2.0f * st);
-        put(1, (y1 + y2) / 2.0f * st);
-        put(2, (x2 - x1) * st);
-        put(3, (y2 - y1) * st);
+        if (p.box) {
+            put(0, (x1 + x2) / 2.0f * st);
+            put(1, (y1 + y2) / 2.0f * st);
+            put(2, (x2 - x1) * st);
+            put(3, (y2 - y1) * st);
+        }
         // class scores: all chunks of a batch of DEC_CB loaded before any is used (a
         // load inside the runtime-bound loop would be waited for one round trip at a time)
         constexpr int DEC_CB = 10;
@@ -477,9 +479,9 @@ __global__ __launch_bounds__(256) void head_decode(const DecodeArgs p) {
     }
     if constexpr (ROWS) {
         __syncthreads();
-        const int rows = 4 + p.nc;
+        const int r0 = p.box ? 0 : 4, rows = 4 + p.nc - r0;
         for (int c = threadIdx.x; c < rows * 32; c += 256) {
-            const int r = c >> 5, k = c & 31;
+            const int r = r0 + (c >> 5), k = c & 31;
             const int a8 = a0 + 8 * k;
             if (a8 >= p.A) continue;
             const T* srow = tile + r * 256 + 8 * k;
@@ -501,11 +503,13 @@ __global__ __launch_bounds__(256) void head_decode(const DecodeArgs p) {
 // each thread decodes its anchor from LDS into registers, and the (4 + nc) x 256
 // output tile, written over the input tile, leaves as 512-B row runs.
 constexpr int DEC_A = 256;
-template <typename T, int NCC>   // NCC = nc / 8 class chunks
+// BOX = false: class rows only (the box rows come from box_dfl), anchors [a_lo, A).
+template <typename T, int NCC, bool BOX>   // NCC = nc / 8 class chunks
 __global__ __launch_bounds__(256, 2) void head_decode_lds(const DecodeArgs p) {
     extern __shared__ __attribute__((aligned(16))) uint4 dsm4[];
-    constexpr int CH = 8 + NCC, CHP = CH + 1;   // chunks per anchor, padded LDS row
-    const int n = blockIdx.y, a0 = blockIdx.x * DEC_A;
+    constexpr int CB = BOX ? 8 : 0;              // box chunks per anchor
+    constexpr int CH = CB + NCC, CHP = CH + 1;   // chunks per anchor, padded LDS row
+    const int n = blockIdx.y, a0 = p.a_lo + blockIdx.x * DEC_A;
     const int tid = threadIdx.x;
     const int l0 = p.H[0] * p.W[0], l1 = p.H[1] * p.W[1];
     auto src_of = [&](int a) {   // first chunk of anchor a of image n
@@ -526,7 +530,7 @@ __global__ __launch_bounds__(256, 2) void head_decode_lds(const DecodeArgs p) {
                 const int ai = q / CH, c = q - ai * CH;
                 const int a = min(a0 + ai, p.A - 1);
                 dst[u] = q < total ? ai * CHP + c : -1;
-                r[u] = q < total ? src_of(a)[c] : make_uint4(0, 0, 0, 0);
+                r[u] = q < total ? src_of(a)[c + 8 - CB] : make_uint4(0, 0, 0, 0);
             }
 #pragma unroll
             for (int u = 0; u < BATCH; ++u)
@@ -541,9 +545,9 @@ __global__ __launch_bounds__(256, 2) void head_decode_lds(const DecodeArgs p) {
     const int W = p.W[l];
     const int gy = loc / W, gx = loc - gy * W;
     const uint4* row = dsm4 + tid * CHP;
-    float dist[4];
+    float dist[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int sd = 0; sd < 4; ++sd) {
+    for (int sd = 0; sd < (BOX ? 4 : 0); ++sd) {
         float v[16];
 #pragma unroll
         for (int c = 0; c < 2; ++c) {
@@ -567,16 +571,18 @@ __global__ __launch_bounds__(256, 2) void head_decode_lds(const DecodeArgs p) {
     }
     uint4 cls[NCC];
 #pragma unroll
-    for (int c = 0; c < NCC; ++c) cls[c] = row[8 + c];
+    for (int c = 0; c < NCC; ++c) cls[c] = row[CB + c];
     __syncthreads();           // the input tile is dead: the output tile reuses it
     T* tile = reinterpret_cast<T*>(dsm4);   // [(4 + nc)][DEC_A]
     const float ax = (float)gx + 0.5f, ay = (float)gy + 0.5f, st = p.stride[l];
     const float x1 = ax - dist[0], y1 = ay - dist[1];
     const float x2 = ax + dist[2], y2 = ay + dist[3];
-    tile[0 * DEC_A + tid] = fromf<T>((x1 + x2) / 2.0f * st);
-    tile[1 * DEC_A + tid] = fromf<T>((y1 + y2) / 2.0f * st);
-    tile[2 * DEC_A + tid] = fromf<T>((x2 - x1) * st);
-    tile[3 * DEC_A + tid] = fromf<T>((y2 - y1) * st);
+    if constexpr (BOX) {
+        tile[0 * DEC_A + tid] = fromf<T>((x1 + x2) / 2.0f * st);
+        tile[1 * DEC_A + tid] = fromf<T>((y1 + y2) / 2.0f * st);
+        tile[2 * DEC_A + tid] = fromf<T>((x2 - x1) * st);
+        tile[3 * DEC_A + tid] = fromf<T>((y2 - y1) * st);
+    }
 #pragma unroll
     for (int c = 0; c < NCC; ++c) {
         Chunk<T> ch;
@@ -588,9 +594,10 @@ __global__ __launch_bounds__(256, 2) void head_decode_lds(const DecodeArgs p) {
     }
     __syncthreads();
     T* yimg = reinterpret_cast<T*>(const_cast<void*>(p.io[1])) + (long long)n * (4 + p.nc) * p.A;
-    const int rows = 4 + p.nc;
+    constexpr int R0 = BOX ? 0 : 4;
+    const int rows = 4 + p.nc - R0;
     for (int c = tid; c < rows * (DEC_A / 8); c += 256) {
-        const int r = c / (DEC_A / 8), k = c - r * (DEC_A / 8);
+        const int r = R0 + c / (DEC_A / 8), k = c - (r - R0) * (DEC_A / 8);
         const int a8 = a0 + 8 * k;
         if (a8 >= p.A) continue;
         const T* srow = tile + r * DEC_A + 8 * k;
@@ -602,25 +609,27 @@ __global__ __launch_bounds__(256, 2) void head_decode_lds(const DecodeArgs p) {
 
 template <typename T>
 int launch_decode_t(const DecodeArgs& a, hipStream_t s) {
-    const dim3 g((unsigned)((a.A + 255) / 256), (unsigned)a.B);
+    if (a.a_lo < 0 || a.a_lo >= a.A || (!a.box && sizeof(T) != 2)) return (int)hipErrorInvalidValue;
+    const dim3 g((unsigned)((a.A - a.a_lo + 255) / 256), (unsigned)a.B);
     if constexpr (sizeof(T) == 2) {
         // instantiated for the 80-class heads (COCO); other class counts take head_decode
         constexpr int NCC = 10;
-        if (a.nc == 8 * NCC && a.A % 8 == 0 && a.ldc % 8 == 0 && a.ldc >= 64 + a.nc) {
-            const int lds_in = DEC_A * (8 + NCC + 1) * 16, lds_out = (4 + a.nc) * DEC_A * 2;
+        if (a.nc == 8 * NCC && a.A % 8 == 0 && a.a_lo % 8 == 0 && a.ldc % 8 == 0 && a.ldc >= 64 + a.nc) {
+            const int lds_in = DEC_A * ((a.box ? 8 : 0) + NCC + 1) * 16, lds_out = (4 + a.nc) * DEC_A * 2;
             const int lds = lds_in > lds_out ? lds_in : lds_out;
-            static bool attr_set = false;
-            if (!attr_set) {
-                (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&head_decode_lds<T, NCC>),
+            auto kern = a.box ? &head_decode_lds<T, NCC, true> : &head_decode_lds<T, NCC, false>;
+            static bool attr_set[2] = {false, false};
+            if (!attr_set[a.box != 0]) {
+                (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
                                           hipFuncAttributeMaxDynamicSharedMemorySize, 80 * 1024);
-                attr_set = true;
+                attr_set[a.box != 0] = true;
             }
-            hipLaunchKernelGGL((head_decode_lds<T, NCC>), g, dim3(256), lds, s, a);
+            hipLaunchKernelGGL(kern, g, dim3(256), lds, s, a);
             return (int)hipGetLastError();
         }
     }
     const int lds = (4 + a.nc) * 256 * (int)sizeof(T);
-    if (a.A % 8 == 0 && lds <= 64 * 1024) {
+    if (a.A % 8 == 0 && a.a_lo % 8 == 0 && lds <= 64 * 1024) {
         hipLaunchKernelGGL((head_decode<T, true>), g, dim3(256), lds, s, a);
     } else {
         hipLaunchKernelGGL((head_decode<T, false>), g, dim3(256), 0, s, a);
