@@ -11,7 +11,7 @@ OBJDIR := build/obj
 HIPFLAGS := --offload-arch=$(ARCH) -O3 -fPIC -std=c++17 -Iinclude -I$(SRC) \
             -fhip-fp32-correctly-rounded-divide-sqrt -Wno-unused-result
 OBJS := $(OBJDIR)/engine.o $(OBJDIR)/conv.o $(OBJDIR)/misc.o $(OBJDIR)/nms.o $(OBJDIR)/conv_mx.o $(OBJDIR)/nms_host.o \
-        $(OBJDIR)/preprocess.o $(OBJDIR)/head.o
+        $(OBJDIR)/preprocess.o $(OBJDIR)/head.o $(OBJDIR)/c3k2.o
 
 all: $(OUT)
 
@@ -34,6 +34,9 @@ $(OBJDIR)/nms_host.o: $(SRC)/nms_host.cpp include/yolo_hip.h | $(OBJDIR)
 	$(HIPCC) $(HIPFLAGS) -x hip -c $< -o $@
 
 $(OBJDIR)/head.o: $(SRC)/head.hip $(SRC)/common.h $(SRC)/dtypes.h | $(OBJDIR)
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+$(OBJDIR)/c3k2.o: $(SRC)/c3k2.hip $(SRC)/common.h $(SRC)/dtypes.h | $(OBJDIR)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
 $(OBJDIR)/preprocess.o: $(SRC)/preprocess.hip $(SRC)/common.h include/yolo_hip.h | $(OBJDIR)

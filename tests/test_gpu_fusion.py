@@ -6,7 +6,9 @@ FMA chains, conv_mx's K order on v_mfma_f32_32x32x16, one rounding per layer out
 head output must be exactly equal with fusion on (default) and off (YH_FUSE=0 at handle
 creation), for every shape: whole and partial tiles, every level, both 16-bit dtypes. The same holds
 for the folded decode (box_dfl writes the box rows, head_cls or a class-rows decode the
-scores), including anchor counts that are not a multiple of 8 (96 x 160: A = 315).
+scores), including anchor counts that are not a multiple of 8 (96 x 160: A = 315), and for
+the fused C3k2 blocks (c3k2.hip: conv1 -> Residual -> conv2 in one launch), whole and
+partial tiles.
 """
 import os
 
@@ -46,6 +48,8 @@ def test_fused_head_equals_per_layer_launches(gpu, variant, dtype, batch, h, w):
     kinds_p = {o["cls"] for o in plain.ops(batch, h, w)}
     assert "head_cls" not in kinds_p and "box_dfl" not in kinds_p
     assert "box_dfl" in kinds_f   # decode folded into the box tail (+ head_cls / class-rows decode)
+    if variant in ("n", "s"):   # C3k2 blocks with one Residual: net.p2.1 (n, s), net.p3.1 (n)
+        assert "c3k2" in kinds_f and "c3k2" not in kinds_p
     if variant == "n":   # s (128) / x (384) cls branches keep the per-layer launches
         assert "head_cls" in kinds_f
         assert len(fused.ops(batch, h, w)) < len(plain.ops(batch, h, w))

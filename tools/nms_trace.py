@@ -28,6 +28,13 @@ def main():
     y = eng.forward(x)
     for _ in range(3):
         nms(y)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(20):
+        nms(y)
+    e1.record()
+    torch.cuda.synchronize()
+    print(f"nms (emit + image) per batch of {B}: {e0.elapsed_time(e1) / 20 * 1e3:.1f} us (HIP events, back to back)")
     tr = torch.zeros((B, 16), dtype=torch.int64, device=dev)
     lib().yh_debug_nms_trace(ctypes.c_void_p(tr.data_ptr()))
     nms(y)

@@ -152,6 +152,31 @@ struct BoxDflArgs {
     int nlv, B, nk, nc, A;
     const void* const* io;
 };
+// Fused C3k2 block with one Residual bottleneck (nets/nn.py:66-80 with n = 1 and
+// csp = False; Residual nn.py:42-49): conv1 1x1 (Cin -> 2c) -> split [a | b] ->
+// b + conv3x3(conv3x3(b)) (c -> c/2 -> c) -> cat [a | b | r] -> conv2 1x1 (3c -> cout),
+// every Conv with SiLU. A persistent workgroup walks TH x TW output tiles; the input tile
+// (2-pixel halo) and every intermediate stay in LDS, the packed weights too. Bit-identical
+// to the four conv_mx launches (same K order, one rounding per layer output, the residual
+// added after the rounding and rounded again).
+struct CspArgs {
+    const void* x; int ldx;          // block input (NHWC view), Cin = 16 * ni channels
+    void* y; int ldy;                // block output view, cout = 32 * no channels
+    int H, W, B;
+    const void* prm;                 // packed weight fragments + fp32 biases (csp_prm_bytes)
+    int ni, nc, no;                  // Cin / 16, c / 16, cout / 32
+    int TH, TW, ntw, tiles, ntiles;  // output tile, tiles per row / per image / in total
+    const void* zero;                // >= 16 zero bytes
+};
+constexpr int CSP_THREADS = 512;
+// bytes of the packed parameter image (weight fragments in MFMA lane order + biases)
+int csp_prm_bytes(int ni, int nc, int no);
+// byte offsets of the parameter image: w1, w2, w3, w4 (fragments), b1, b2, b3, b4 (fp32), total
+void csp_offsets(int ni, int nc, int no, int (&off)[9]);
+// LDS bytes for a TH x TW tile, 0 if it does not fit or (ni, nc, no) is not instantiated
+int csp_lds(int TH, int TW, int ni, int nc, int no);
+int launch_csp(int dtype, const CspArgs& a, int grid, hipStream_t s);
+
 constexpr int BOX_DFL_TPW = 4;       // 32-pixel tiles per wave (4 waves per workgroup)
 int launch_box_dfl(int dtype, const BoxDflArgs& a, hipStream_t s);
 

@@ -89,9 +89,9 @@ static uint16_t f2h(float f) {
 
 // ---------------------------------------------------------------- graph model
 enum ConvKind { CK_DENSE = 0, CK_FIRST = 1, CK_DW = 2, CK_PE = 3 };
-enum OpKind { OP_FIRST, OP_CONV, OP_DW, OP_SPPF, OP_ATTN, OP_DECODE, OP_HEADCLS, OP_BOXDFL };
+enum OpKind { OP_FIRST, OP_CONV, OP_DW, OP_SPPF, OP_ATTN, OP_DECODE, OP_HEADCLS, OP_BOXDFL, OP_CSP };
 enum OpClass { CL_CONV3 = 0, CL_CONV1 = 1, CL_FIRST = 2, CL_DW = 3, CL_SPPF = 4, CL_ATTN = 5, CL_DECODE = 6,
-               CL_HEADCLS = 7, CL_BOXDFL = 8, CL_N = 9 };
+               CL_HEADCLS = 7, CL_BOXDFL = 8, CL_CSP = 9, CL_N = 10 };
 
 struct Tensor { int level; int C; };        // physical channels = pixel stride
 struct View { int t = -1; int coff = 0; int C = 0; };
@@ -133,6 +133,8 @@ struct Op {
     // OP_DECODE: first level decoded, and whether the box rows are (false: box_dfl writes them)
     int dlo = 0;
     bool dbox = true;
+    // OP_CSP: conv1, res_m.0.conv1, res_m.0.conv2, conv2 of a fused C3k2 block (in[0] -> out)
+    int cs[4] = {-1, -1, -1, -1};
     std::string label;
 };
 
@@ -270,6 +272,20 @@ struct Net {
     void csp(const std::string& p, const std::vector<Seg>& in, const std::vector<int>& logical, int out_ch, int n,
              bool use_c3k, int r, View out, int level) {
         const int c = out_ch / r;
+        if (n == 1 && !use_c3k && fuse_csp(in, logical, c, out_ch, out)) {
+            // one launch for the whole block (c3k2.hip); the same four convs, loaded by name
+            Op op;
+            op.kind = OP_CSP;
+            op.label = p;
+            op.cs[0] = new_dense_conv(p + ".conv1", logical[0], 2 * c, 1, 0, ACT_SILU);
+            op.cs[1] = new_dense_conv(p + ".res_m.0.conv1", c, c / 2, 3, 0, ACT_SILU);
+            op.cs[2] = new_dense_conv(p + ".res_m.0.conv2", c / 2, c, 3, 0, ACT_SILU);
+            op.cs[3] = new_dense_conv(p + ".conv2", 3 * c, out_ch, 1, 0, ACT_SILU);
+            op.in = in;
+            op.out = out;
+            ops.push_back(op);
+            return;
+        }
         const int t = tensor(level, (2 + n) * c);
         dense(p + ".conv1", in, logical, 2 * c, 1, 1, ACT_SILU, slice(t, 0, 2 * c));
         for (int i = 0; i < n; ++i) {
@@ -454,6 +470,95 @@ struct Net {
         const int ci = new_conv(name, CK_DENSE, cin, cout, k, 1, 1, has_bias, act);
         convs[ci].segs.push_back({cin, round_up(cin, 8)});
         return ci;
+    }
+    // a C3k2 block with one Residual runs fused (c3k2.hip) on 16-bit handles when its input
+    // is one plain view of 16-channel blocks and (Cin, c, cout) has an instantiated kernel
+    bool fuse_csp(const std::vector<Seg>& in, const std::vector<int>& logical, int c, int out_ch, View out) const {
+        const char* e = getenv("YH_FUSE");
+        if (dtype == F32 || (e && atoi(e) == 0)) return false;
+        const char* e2 = getenv("YH_FUSE_CSP");
+        if (e2 && atoi(e2) == 0) return false;
+        if (in.size() != 1 || in[0].up || in[0].v.C != logical[0] || logical[0] % 16 || c % 16 || out_ch % 32) return false;
+        if (out.coff % 8 || in[0].v.coff % 8) return false;
+        int TH, TW;
+        return csp_tile(logical[0] / 16, c / 16, out_ch / 32, 1 << 30, 1 << 30, TH, TW);
+    }
+    static bool csp_tile(int ni, int nc, int no, int H, int W, int& TH, int& TW) {
+        static const int cand[][2] = {{8, 16}, {8, 8}, {4, 16}, {4, 8}, {2, 8}, {2, 4}};
+        // YH_CSP_TILE=<TH>x<TW> (experiments): preferred tile when it fits
+        static const std::pair<int, int> pref = [] {
+            int a = 0, b = 0;
+            if (const char* e = getenv("YH_CSP_TILE")) sscanf(e, "%dx%d", &a, &b);
+            return std::make_pair(a, b);
+        }();
+        if (pref.first > 0 && pref.first <= H && pref.second <= W && csp_lds(pref.first, pref.second, ni, nc, no) > 0) {
+            TH = pref.first;
+            TW = pref.second;
+            return true;
+        }
+        for (auto& c : cand) {
+            if (c[0] > H || c[1] > W) continue;
+            if (csp_lds(c[0], c[1], ni, nc, no) > 0) {
+                TH = c[0];
+                TW = c[1];
+                return true;
+            }
+        }
+        return false;
+    }
+    // packed parameter image of a fused C3k2 op (cached in conv1's mx_w; the other three
+    // convs hold a marker, so reloading any of the four rebuilds it)
+    const void* csp_params(const Op& op) {
+        ConvDesc& d0 = convs[op.cs[0]];
+        auto it = d0.mx_w.find("csp");
+        bool ok = it != d0.mx_w.end();
+        for (int k = 1; k < 4; ++k) ok = ok && convs[op.cs[k]].mx_w.count("csp_dep");
+        if (ok) return it->second;
+        if (it != d0.mx_w.end()) {
+            (void)hipFree(it->second);
+            d0.mx_w.erase(it);
+        }
+        for (int k = 0; k < 4; ++k) require(convs[op.cs[k]].loaded, "weights of " + convs[op.cs[k]].name + " not loaded", YH_ESTATE);
+        const ConvDesc &c1 = convs[op.cs[0]], &r1 = convs[op.cs[1]], &r2 = convs[op.cs[2]], &c2 = convs[op.cs[3]];
+        const int ni = c1.cin / 16, nc = r1.cin / 16, no = c2.cout / 32, nh = (nc + 1) / 2;
+        int off[9];
+        csp_offsets(ni, nc, no, off);
+        std::vector<uint8_t> img((size_t)off[8], 0);
+        // fragment (tile a, step k, lane, j): cout row permuted so lane half hh holds couts
+        // 32a + 16hh .. +15; K value 8hh + j of step k = (block cb, tap)
+        auto frags = [&](int o, const ConvDesc& d, int ntile, int nk) {
+            const int kk2 = d.k * d.k;
+            uint16_t* dst = reinterpret_cast<uint16_t*>(img.data() + o);
+            for (int a = 0; a < ntile; ++a)
+                for (int k = 0; k < nk; ++k)
+                    for (int lane = 0; lane < 64; ++lane)
+                        for (int j = 0; j < 8; ++j) {
+                            const int R = lane & 31, hh = lane >> 5;
+                            const int co = 32 * a + 16 * ((R >> 2) & 1) + (R & 3) + 4 * (R >> 3);
+                            const int cb = k / kk2, tap = k - cb * kk2, ch = 16 * cb + 8 * hh + j;
+                            float v = 0.f;
+                            if (co < d.cout && ch < d.cin) v = d.wf[((size_t)co * d.cin + ch) * kk2 + tap];
+                            dst[((size_t)(a * nk + k) * 64 + lane) * 8 + j] = dtype == BF16 ? f2bf(v) : f2h(v);
+                        }
+        };
+        frags(off[0], c1, nc, ni);
+        frags(off[1], r1, 1, 9 * nc);
+        frags(off[2], r2, nh, 9 * nh);
+        frags(off[3], c2, no, 3 * nc);
+        auto biases = [&](int o, const ConvDesc& d) {
+            float* dst = reinterpret_cast<float*>(img.data() + o);
+            for (int i = 0; i < d.cout; ++i) dst[i] = d.bf[i];
+        };
+        biases(off[4], c1);
+        biases(off[5], r1);
+        biases(off[6], r2);
+        biases(off[7], c2);
+        void* dev = nullptr;
+        HIPCHECK(hipMalloc(&dev, img.size()));
+        HIPCHECK(hipMemcpy(dev, img.data(), img.size(), hipMemcpyHostToDevice));
+        d0.mx_w.emplace("csp", dev);
+        for (int k = 1; k < 4; ++k) convs[op.cs[k]].mx_w.emplace("csp_dep", nullptr);
+        return dev;
     }
     // the decode folds into box_dfl + head_cls / a class-rows decode (16-bit handles; the
     // box branch's last conv has 4 or 6 16-channel K blocks)
@@ -1056,6 +1161,32 @@ struct Net {
                 break;
             }
             case OP_BOXDFL: rc = launch_box_dfl(dtype, box_dfl_args(op, B, H, W), s); break;
+            case OP_CSP: {
+                CspArgs a{};
+                const View& xv = op.in[0].v;
+                const int lv = tensors[xv.t].level;
+                a.x = ptr(xv);
+                a.ldx = ldc(xv);
+                a.y = ptr(op.out);
+                a.ldy = ldc(op.out);
+                a.H = H >> lv;
+                a.W = W >> lv;
+                a.B = B;
+                a.prm = csp_params(op);
+                a.ni = convs[op.cs[0]].cin / 16;
+                a.nc = convs[op.cs[1]].cin / 16;
+                a.no = convs[op.cs[3]].cout / 32;
+                require(csp_tile(a.ni, a.nc, a.no, a.H, a.W, a.TH, a.TW), op.label + ": no LDS tile");
+                a.ntw = (a.W + a.TW - 1) / a.TW;
+                a.tiles = a.ntw * ((a.H + a.TH - 1) / a.TH);
+                a.ntiles = B * a.tiles;
+                a.zero = zero_dev;
+                if (!num_cus) HIPCHECK(hipDeviceGetAttribute(&num_cus, hipDeviceAttributeMultiprocessorCount, device));
+                // two workgroups per CU when the LDS allows (measured: net.p2.1 138 -> 103 us at b32)
+                static const int per_cu = [] { const char* e = getenv("YH_CSP_WG_PER_CU"); return e ? atoi(e) : 2; }();
+                rc = launch_csp(dtype, a, std::min(a.ntiles, per_cu * num_cus), s);
+                break;
+            }
         }
         if (rc != 0) throw Fail(YH_EHIP, "launch of " + op.label + " failed: " + hipGetErrorString((hipError_t)rc));
     }
@@ -1183,6 +1314,7 @@ struct Net {
             case OP_DECODE: return CL_DECODE;
             case OP_HEADCLS: return CL_HEADCLS;
             case OP_BOXDFL: return CL_BOXDFL;
+            case OP_CSP: return CL_CSP;
         }
         return CL_CONV1;
     }
@@ -1259,6 +1391,18 @@ struct Net {
                     for (int l = op.dlo; l < 3; ++l) A += px(tensors[op.lvl[l].t].level);
                     bytes = 2.0 * A * var.num_classes * es;
                     flops = A * var.num_classes * 4.0;
+                }
+                break;
+            }
+            case OP_CSP: {
+                // block input read once, block output written once, the four convs' weights once
+                const ConvDesc &c1 = convs[op.cs[0]], &r1 = convs[op.cs[1]], &r2 = convs[op.cs[2]], &c2 = convs[op.cs[3]];
+                const double n = px(tensors[op.out.t].level);
+                bytes = n * c1.cin * es + n * c2.cout * es;
+                for (const ConvDesc* d : {&c1, &r1, &r2, &c2}) {
+                    const double macs = (double)d->cout * d->cin * d->k * d->k;
+                    bytes += macs * es;
+                    flops += 2.0 * n * macs;
                 }
                 break;
             }
@@ -1555,7 +1699,7 @@ int yh_op_kernel(const yh_handle* h, int index, int batch, int height, int width
     return guarded([&] {
         yh::require(h && index >= 0 && index < (int)h->net.ops.size(), "op index out of range");
         const yh::Net& n = h->net;
-        static const char* op_names[] = {"stem", "conv", "dwconv", "sppf", "attention", "decode", "head_cls", "box_dfl"};
+        static const char* op_names[] = {"stem", "conv", "dwconv", "sppf", "attention", "decode", "head_cls", "box_dfl", "c3k2"};
         const yh::Op& op = n.ops[index];
         if (op.kind != yh::OP_CONV) {
             if (name) *name = op_names[(int)op.kind];
