@@ -23,9 +23,17 @@ def main():
                 rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"]))
     rows.sort()
     marks = [i for i, r in enumerate(rows) if "fill" in r[2].lower()]
-    if len(marks) < 2:
+    # a marker is torch.zeros(1) + fill_(v): consecutive fill dispatches form one cluster;
+    # the timed region lies between the last two clusters
+    clusters = []
+    for i in marks:
+        if clusters and i == clusters[-1][-1] + 1:
+            clusters[-1].append(i)
+        else:
+            clusters.append([i])
+    if len(clusters) < 2:
         raise SystemExit("markers not found")
-    a, b = marks[-2], marks[-1]
+    a, b = clusters[-2][-1], clusters[-1][0]
     region = rows[a + 1:b]
     t0, t1 = rows[a][1], rows[b][0]
     stats = {}
