@@ -6,10 +6,10 @@ HIPCC ?= $(ROCM)/bin/hipcc
 ARCH ?= gfx950
 PKG := yolo-infer-pt_amd
 SRC := $(PKG)/csrc
-OUT := $(PKG)/yolo_hip/libyolo_hip.so
-OBJDIR := build/obj
+OUT ?= $(PKG)/yolo_hip/libyolo_hip.so
+OBJDIR ?= build/obj
 HIPFLAGS := --offload-arch=$(ARCH) -O3 -fPIC -std=c++17 -Iinclude -I$(SRC) \
-            -fhip-fp32-correctly-rounded-divide-sqrt -Wno-unused-result
+            -fhip-fp32-correctly-rounded-divide-sqrt -Wno-unused-result $(EXTRA)
 OBJS := $(OBJDIR)/engine.o $(OBJDIR)/conv.o $(OBJDIR)/misc.o $(OBJDIR)/nms.o $(OBJDIR)/conv_mx.o $(OBJDIR)/nms_host.o \
         $(OBJDIR)/preprocess.o $(OBJDIR)/head.o $(OBJDIR)/c3k2.o
 

@@ -168,7 +168,10 @@ struct CspArgs {
     int TH, TW, ntw, tiles, ntiles;  // output tile, tiles per row / per image / in total
     const void* zero;                // >= 16 zero bytes
 };
-constexpr int CSP_THREADS = 512;
+#ifndef YH_CSP_THREADS
+#define YH_CSP_THREADS 512
+#endif
+constexpr int CSP_THREADS = YH_CSP_THREADS;
 // bytes of the packed parameter image (weight fragments in MFMA lane order + biases)
 int csp_prm_bytes(int ni, int nc, int no);
 // byte offsets of the parameter image: w1, w2, w3, w4 (fragments), b1, b2, b3, b4 (fp32), total

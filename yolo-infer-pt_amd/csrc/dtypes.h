@@ -55,7 +55,11 @@ __device__ __forceinline__ Chunk<T> f_to_chunk(const float (&f)[8]) {
 
 // SiLU: exact-rounded exp/div on the f32 (parity) path, hardware exp/rcp on 16-bit paths.
 template <typename T> __device__ __forceinline__ float silu(float x) {
+#ifdef YH_SILU_EXPERIMENT   // cost experiment only (wrong values): SiLU without transcendentals
+    return x * fmaf(x, 0.25f, 0.5f);
+#else
     return x * __builtin_amdgcn_rcpf(1.0f + __expf(-x));
+#endif
 }
 template <> __device__ __forceinline__ float silu<float>(float x) { return x / (1.0f + expf(-x)); }
 

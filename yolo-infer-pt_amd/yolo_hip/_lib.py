@@ -11,6 +11,9 @@ import os
 from ctypes import POINTER, byref, c_char_p, c_double, c_float, c_int, c_size_t, c_void_p
 
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libyolo_hip.so")
+# experiments only: YH_LIB=<path> loads another build of the same library
+if os.environ.get("YH_LIB"):
+    LIB_PATH = os.environ["YH_LIB"]
 
 YH_F32, YH_F16, YH_BF16 = 0, 1, 2
 ABI_VERSION = 2
