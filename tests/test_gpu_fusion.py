@@ -21,17 +21,20 @@ from yolo_hip import synth
 pytestmark = pytest.mark.gpu
 
 
-def _engine(model, dtype, dev, fuse):
+def _engine(model, dtype, dev, fuse, **env):
+    """Engine built with YH_FUSE (and any extra YH_* settings) set at handle creation."""
     from yolo_hip.engine import Engine
-    old = os.environ.get("YH_FUSE")
-    os.environ["YH_FUSE"] = "1" if fuse else "0"
+    env = {"YH_FUSE": "1" if fuse else "0", **env}
+    old = {k: os.environ.get(k) for k in env}
+    os.environ.update(env)
     try:
         eng = Engine(*model._yh_arch, dev, dtype)
     finally:
-        if old is None:
-            del os.environ["YH_FUSE"]
-        else:
-            os.environ["YH_FUSE"] = old
+        for k, v in old.items():
+            if v is None:
+                del os.environ[k]
+            else:
+                os.environ[k] = v
     eng.load_module(model)
     return eng
 
@@ -59,3 +62,18 @@ def test_fused_head_equals_per_layer_launches(gpu, variant, dtype, batch, h, w):
     assert torch.equal(yf, yp), (yf.float() - yp.float()).abs().max().item()
     fused.set_graph(False)
     assert torch.equal(fused.forward(x), yp)
+
+
+@pytest.mark.parametrize("dtype,batch,h,w", [(torch.bfloat16, 2, 640, 640), (torch.float16, 3, 96, 160)])
+def test_csp_tail_mode_equals_per_layer_launches(gpu, dtype, batch, h, w):
+    """C3k2 tail mode (conv1 launched alone, Residual + conv2 fused; the default for
+    fpn.h2's two-segment input) forced on every eligible block of v11_n."""
+    model = make_model("n")
+    x = synth.synth_scenes(batch, h, w, seed=37).to(gpu, dtype)
+    tail = _engine(model, dtype, gpu, True, YH_CSP_TAIL="1")
+    plain = _engine(model, dtype, gpu, False)
+    labels = [o["label"] for o in tail.ops(batch, h, w) if o["cls"] == "c3k2"]
+    assert "net.p3.1.tail" in labels and "fpn.h2.tail" in labels, labels
+    yt = tail.forward(x).clone()
+    yp = plain.forward(x).clone()
+    assert torch.equal(yt, yp), (yt.float() - yp.float()).abs().max().item()

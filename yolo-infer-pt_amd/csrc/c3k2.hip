@@ -104,7 +104,7 @@ __host__ __device__ inline CsTile cs_tile(int TH, int TW, int ni, int nc, int no
     const int XP = (TH + 4) * (TW + 4), MP = (TH + 2) * (TW + 2), NP = TH * TW;
     CsTile t{};
     t.lx = L.prm;
-    t.lt = t.lx + ((XP * (16 * ni + 8) * 2 + 1023) & ~1023);
+    t.lt = t.lx + (ni ? ((XP * (16 * ni + 8) * 2 + 1023) & ~1023) : 0);   // tail mode: no X region
     t.lr = t.lt + XP * (32 * nc + 8) * 2;
     t.lc = t.lr + MP * (16 * nh + 8) * 2;
     t.total = t.lc + NP * (16 * nc + 8) * 2;
@@ -189,7 +189,12 @@ __global__ __launch_bounds__(CSP_THREADS) void csp_fused(const CspArgs A) {
         const char* prm = reinterpret_cast<const char*>(A.prm);
         for (int i0 = wvu * 64; i0 < L.prm / 16; i0 += CSP_THREADS) cs_glds(prm + (size_t)(i0 + lane) * 16, lds0 + i0 * 16);
     }
-    constexpr int CPX = 2 * NI + 1;   // 16-B chunks per stored pixel (the last one is padding)
+    // tail mode (NI == 0): the block input is conv1's output [a | b] (2c channels, computed
+    // by its own launch) and lands straight in T1; P1 is skipped
+    constexpr bool TAIL = NI == 0;
+    constexpr int NCH = TAIL ? 4 * NC : 2 * NI;   // 16-B data chunks per pixel
+    constexpr int CPX = NCH + 1;                  // + one padding chunk per stored pixel
+    const unsigned LD = TAIL ? LT : LX;
     auto load_x = [&](int t) {
         const int n = t / A.tiles, tix = t - n * A.tiles;
         const int ty = tix / A.ntw, tx = tix - ty * A.ntw;
@@ -200,9 +205,9 @@ __global__ __launch_bounds__(CSP_THREADS) void csp_fused(const CspArgs A) {
             const int px = q / CPX, c = q - px * CPX;
             const int r = px / XW, cc = px - r * XW;
             const int gh = h0 + r, gw = w0 + cc;
-            const bool ok = q < total && c < 2 * NI && (unsigned)gh < (unsigned)A.H && (unsigned)gw < (unsigned)A.W;
+            const bool ok = q < total && c < NCH && (unsigned)gh < (unsigned)A.H && (unsigned)gw < (unsigned)A.W;
             const void* src = ok ? (const void*)(x + (((long long)n * A.H + gh) * A.W + gw) * A.ldx + c * 8) : A.zero;
-            cs_glds(src, LX + i0 * 16);
+            cs_glds(src, LD + i0 * 16);
         }
     };
     if ((int)blockIdx.x < A.ntiles) load_x(blockIdx.x);
@@ -215,6 +220,7 @@ __global__ __launch_bounds__(CSP_THREADS) void csp_fused(const CspArgs A) {
         cs_barrier();
 
         // P1: conv1 over the halo tile, X -> T1 (zero outside the image)
+        if constexpr (!TAIL) {
         cs_phase<T, NC, NI>(
                 lds0 + L.w1, XP,
                 [&](int px, int k) { return LX + (unsigned)(px * SX + 16 * k + 8 * hh) * 2; },
@@ -230,6 +236,7 @@ __global__ __launch_bounds__(CSP_THREADS) void csp_fused(const CspArgs A) {
                 });
         cs_barrier();
         if (t + (int)gridDim.x < A.ntiles) load_x(t + gridDim.x);   // X is dead: next tile's input
+        }
 
         // P2: Residual conv1 (3x3, b -> R1) over the 1-pixel halo region
         cs_phase<T, 1, 9 * NC>(
@@ -303,12 +310,17 @@ __global__ __launch_bounds__(CSP_THREADS) void csp_fused(const CspArgs A) {
                         d[1] = o[1];
                     }
                 });
+        if constexpr (TAIL) {   // T1 is read until here: the next tile's input after a barrier
+            cs_barrier();
+            if (t + (int)gridDim.x < A.ntiles) load_x(t + gridDim.x);
+        }
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
-// instantiated (ni, nc, no): v11_n p2.1 (2, 1, 2), p3.1 and v11_s p2.1 (4, 2, 4)
-#define YH_CSP_LIST(X) X(2, 1, 2) X(4, 2, 4)
+// instantiated (ni, nc, no): v11_n p2.1 (2, 1, 2), p3.1 and v11_s p2.1 (4, 2, 4); tail mode
+// (ni = 0): v11_n fpn.h2 (0, 2, 2), p3.1 (0, 2, 4)
+#define YH_CSP_LIST(X) X(2, 1, 2) X(4, 2, 4) X(0, 2, 2) X(0, 2, 4)
 
 template <typename T>
 int launch_csp_t(const CspArgs& a, int grid, hipStream_t s) {

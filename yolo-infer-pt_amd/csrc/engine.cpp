@@ -272,6 +272,24 @@ struct Net {
     void csp(const std::string& p, const std::vector<Seg>& in, const std::vector<int>& logical, int out_ch, int n,
              bool use_c3k, int r, View out, int level) {
         const int c = out_ch / r;
+        const bool tail = n == 1 && !use_c3k && fuse_csp_tail(c, out_ch, out) &&
+                          (tail_first() || !fuse_csp(in, logical, c, out_ch, out));
+        if (tail) {
+            // conv1 as its own launch into a compact [a | b] tensor, then Residual + conv2 as
+            // one launch (c3k2.hip tail mode)
+            const int t1 = tensor(level, 2 * c);
+            dense(p + ".conv1", in, logical, 2 * c, 1, 1, ACT_SILU, full(t1));
+            Op op;
+            op.kind = OP_CSP;
+            op.label = p + ".tail";
+            op.cs[1] = new_dense_conv(p + ".res_m.0.conv1", c, c / 2, 3, 0, ACT_SILU);
+            op.cs[2] = new_dense_conv(p + ".res_m.0.conv2", c / 2, c, 3, 0, ACT_SILU);
+            op.cs[3] = new_dense_conv(p + ".conv2", 3 * c, out_ch, 1, 0, ACT_SILU);
+            op.in = {Seg{full(t1, 2 * c), 0}};
+            op.out = out;
+            ops.push_back(op);
+            return;
+        }
         if (n == 1 && !use_c3k && fuse_csp(in, logical, c, out_ch, out)) {
             // one launch for the whole block (c3k2.hip); the same four convs, loaded by name
             Op op;
@@ -483,6 +501,20 @@ struct Net {
         int TH, TW;
         return csp_tile(logical[0] / 16, c / 16, out_ch / 32, 1 << 30, 1 << 30, TH, TW);
     }
+    bool fuse_csp_tail(int c, int out_ch, View out) const {
+        const char* e = getenv("YH_FUSE");
+        if (dtype == F32 || (e && atoi(e) == 0)) return false;
+        const char* e2 = getenv("YH_FUSE_CSP");
+        if (e2 && atoi(e2) == 0) return false;
+        if (c % 16 || out_ch % 32 || out.coff % 8) return false;
+        int TH, TW;
+        return csp_tile(0, c / 16, out_ch / 32, 1 << 30, 1 << 30, TH, TW);
+    }
+    // YH_CSP_TAIL=1 (experiments): tail mode even where the whole block fits one launch
+    static bool tail_first() {
+        const char* e = getenv("YH_CSP_TAIL");
+        return e && atoi(e) != 0;
+    }
     static bool csp_tile(int ni, int nc, int no, int H, int W, int& TH, int& TW) {
         static const int cand[][2] = {{8, 16}, {8, 8}, {4, 16}, {4, 8}, {2, 8}, {2, 4}};
         // YH_CSP_TILE=<TH>x<TW> (experiments): preferred tile when it fits
@@ -496,31 +528,38 @@ struct Net {
             TW = pref.second;
             return true;
         }
-        for (auto& c : cand) {
-            if (c[0] > H || c[1] > W) continue;
-            if (csp_lds(c[0], c[1], ni, nc, no) > 0) {
-                TH = c[0];
-                TW = c[1];
-                return true;
+        // the largest tile of >= 64 pixels that leaves room for a second workgroup per CU,
+        // else the largest that fits (measured: net.p3.1 at 2x4 tiles, two per CU, 263 us
+        // against 68 us at 8x16, one per CU)
+        for (int lim : {80 * 1024, 160 * 1024})
+            for (auto& c : cand) {
+                if (c[0] > H || c[1] > W || (lim == 80 * 1024 && c[0] * c[1] < 64)) continue;
+                const int b = csp_lds(c[0], c[1], ni, nc, no);
+                if (b > 0 && b <= lim) {
+                    TH = c[0];
+                    TW = c[1];
+                    return true;
+                }
             }
-        }
         return false;
     }
     // packed parameter image of a fused C3k2 op (cached in conv1's mx_w; the other three
     // convs hold a marker, so reloading any of the four rebuilds it)
     const void* csp_params(const Op& op) {
-        ConvDesc& d0 = convs[op.cs[0]];
+        // tail mode (no conv1 in the op): the cache lives in the Residual's first conv
+        const int k0 = op.cs[0] >= 0 ? 0 : 1;
+        ConvDesc& d0 = convs[op.cs[k0]];
         auto it = d0.mx_w.find("csp");
         bool ok = it != d0.mx_w.end();
-        for (int k = 1; k < 4; ++k) ok = ok && convs[op.cs[k]].mx_w.count("csp_dep");
+        for (int k = k0 + 1; k < 4; ++k) ok = ok && convs[op.cs[k]].mx_w.count("csp_dep");
         if (ok) return it->second;
         if (it != d0.mx_w.end()) {
             (void)hipFree(it->second);
             d0.mx_w.erase(it);
         }
-        for (int k = 0; k < 4; ++k) require(convs[op.cs[k]].loaded, "weights of " + convs[op.cs[k]].name + " not loaded", YH_ESTATE);
-        const ConvDesc &c1 = convs[op.cs[0]], &r1 = convs[op.cs[1]], &r2 = convs[op.cs[2]], &c2 = convs[op.cs[3]];
-        const int ni = c1.cin / 16, nc = r1.cin / 16, no = c2.cout / 32, nh = (nc + 1) / 2;
+        for (int k = k0; k < 4; ++k) require(convs[op.cs[k]].loaded, "weights of " + convs[op.cs[k]].name + " not loaded", YH_ESTATE);
+        const ConvDesc &r1 = convs[op.cs[1]], &r2 = convs[op.cs[2]], &c2 = convs[op.cs[3]];
+        const int ni = k0 == 0 ? convs[op.cs[0]].cin / 16 : 0, nc = r1.cin / 16, no = c2.cout / 32, nh = (nc + 1) / 2;
         int off[9];
         csp_offsets(ni, nc, no, off);
         std::vector<uint8_t> img((size_t)off[8], 0);
@@ -541,7 +580,7 @@ struct Net {
                             dst[((size_t)(a * nk + k) * 64 + lane) * 8 + j] = dtype == BF16 ? f2bf(v) : f2h(v);
                         }
         };
-        frags(off[0], c1, nc, ni);
+        if (ni) frags(off[0], convs[op.cs[0]], nc, ni);
         frags(off[1], r1, 1, 9 * nc);
         frags(off[2], r2, nh, 9 * nh);
         frags(off[3], c2, no, 3 * nc);
@@ -549,7 +588,7 @@ struct Net {
             float* dst = reinterpret_cast<float*>(img.data() + o);
             for (int i = 0; i < d.cout; ++i) dst[i] = d.bf[i];
         };
-        biases(off[4], c1);
+        if (ni) biases(off[4], convs[op.cs[0]]);
         biases(off[5], r1);
         biases(off[6], r2);
         biases(off[7], c2);
@@ -557,7 +596,7 @@ struct Net {
         HIPCHECK(hipMalloc(&dev, img.size()));
         HIPCHECK(hipMemcpy(dev, img.data(), img.size(), hipMemcpyHostToDevice));
         d0.mx_w.emplace("csp", dev);
-        for (int k = 1; k < 4; ++k) convs[op.cs[k]].mx_w.emplace("csp_dep", nullptr);
+        for (int k = k0 + 1; k < 4; ++k) convs[op.cs[k]].mx_w.emplace("csp_dep", nullptr);
         return dev;
     }
     // the decode folds into box_dfl + head_cls / a class-rows decode (16-bit handles; the
@@ -1173,7 +1212,7 @@ struct Net {
                 a.W = W >> lv;
                 a.B = B;
                 a.prm = csp_params(op);
-                a.ni = convs[op.cs[0]].cin / 16;
+                a.ni = op.cs[0] >= 0 ? convs[op.cs[0]].cin / 16 : 0;
                 a.nc = convs[op.cs[1]].cin / 16;
                 a.no = convs[op.cs[3]].cout / 32;
                 require(csp_tile(a.ni, a.nc, a.no, a.H, a.W, a.TH, a.TW), op.label + ": no LDS tile");
@@ -1396,10 +1435,11 @@ struct Net {
             }
             case OP_CSP: {
                 // block input read once, block output written once, the four convs' weights once
-                const ConvDesc &c1 = convs[op.cs[0]], &r1 = convs[op.cs[1]], &r2 = convs[op.cs[2]], &c2 = convs[op.cs[3]];
                 const double n = px(tensors[op.out.t].level);
-                bytes = n * c1.cin * es + n * c2.cout * es;
-                for (const ConvDesc* d : {&c1, &r1, &r2, &c2}) {
+                bytes = n * op.in[0].v.C * es + n * convs[op.cs[3]].cout * es;
+                for (int k = 0; k < 4; ++k) {
+                    if (op.cs[k] < 0) continue;   // tail mode: conv1 is its own op
+                    const ConvDesc* d = &convs[op.cs[k]];
                     const double macs = (double)d->cout * d->cin * d->k * d->k;
                     bytes += macs * es;
                     flops += 2.0 * n * macs;
