@@ -642,7 +642,7 @@ __global__ __launch_bounds__(64 * NW, 2) void conv_mxr(const MxArgs p) {
 #pragma unroll
         for (int i = 0; i < NBI; ++i) {
             const int c = (slot_geo[i] >> 22) & 15;
-            const bool ok = sptr[i] != nullptr && c < clim;
+            const bool ok = sptr[i] != nullptr && c < clim && !(p.dbg & 2);
             mx_glds(ok ? (const void*)(sptr[i] + coff) : (const void*)p.zero, bb + (unsigned)(i * 1024));
         }
     };
@@ -711,7 +711,7 @@ __global__ __launch_bounds__(64 * NW, 2) void conv_mxr(const MxArgs p) {
             for (int a = 0; a < NA; ++a) aj[a] = acc[a][j];
             T* op = out + m * p.ldo + cc;
             const T* rp = res + m * p.ldr + cc;
-            if (p.act == ACT_SILU) {
+            if (p.act == ACT_SILU && !(p.dbg & 16)) {
                 if (res) mx_epi<T, NA, true, true>(aj, bv, op, rp, nc8);
                 else mx_epi<T, NA, true, false>(aj, bv, op, rp, nc8);
             } else {
@@ -722,12 +722,17 @@ __global__ __launch_bounds__(64 * NW, 2) void conv_mxr(const MxArgs p) {
     };
 
     const int nstages = (t_hi - t_lo) * p.nst;
+    if ((p.dbg & 64) && __builtin_amdgcn_readfirstlane(threadIdx.x) >= 32 * NW) __builtin_amdgcn_s_setprio(1);
     issue(0);
     for (int g = 0; g < nstages; ++g) {
         const bool more = g + 1 < nstages;
+        const bool after_epi = g > 0 && (g - (g / p.nst) * p.nst) == 0;
         if (NBUF == 2 && more) {
             issue(g + 1);
-            asm volatile("s_waitcnt vmcnt(%0)" :: "n"(NBI) : "memory");
+            if ((p.dbg & 32) && after_epi)
+                asm volatile("s_waitcnt vmcnt(%0)" :: "n"(NBI + 2 * NA * MB) : "memory");
+            else
+                asm volatile("s_waitcnt vmcnt(%0)" :: "n"(NBI) : "memory");
         } else {
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         }
@@ -740,10 +745,10 @@ __global__ __launch_bounds__(64 * NW, 2) void conv_mxr(const MxArgs p) {
 #pragma unroll
                     for (int e = 0; e < 16; ++e) acc[a][j][e] = 0.f;
         }
-        compute(g);
+        if (!(p.dbg & 4)) compute(g);
         // single buffer: the next stage's DMA may only start once this stage's reads are done
         if (NBUF == 1 && more) issue(g + 1);
-        if (st == p.nst - 1) epilogue(t_lo + g / p.nst);
+        if (st == p.nst - 1 && !(p.dbg & 8)) epilogue(t_lo + g / p.nst);
     }
 }
 
