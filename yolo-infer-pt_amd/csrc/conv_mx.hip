@@ -509,8 +509,9 @@ __global__ __launch_bounds__(64 * NW, 2) void conv_mxr(const MxArgs p) {
     // ---- resident weights + bias
     {
         const char* wsrc = p.w + (long long)sl * p.wstage;
-        for (int q = wv * 64; q < wch; q += 64 * NW)   // wch: a multiple of 64 chunks
-            mx_glds(wsrc + (long long)(q + lane) * 16, lds0 + (unsigned)q * 16);
+        if (!(p.dbg & 1024))
+            for (int q = wv * 64; q < wch; q += 64 * NW)   // wch: a multiple of 64 chunks
+                mx_glds(wsrc + (long long)(q + lane) * 16, lds0 + (unsigned)q * 16);
         if (threadIdx.x < BN / 4)
             sm4[bias_ch + threadIdx.x] = *reinterpret_cast<const uint4*>(p.bias + sl * BN + threadIdx.x * 4);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -722,17 +723,12 @@ __global__ __launch_bounds__(64 * NW, 2) void conv_mxr(const MxArgs p) {
     };
 
     const int nstages = (t_hi - t_lo) * p.nst;
-    if ((p.dbg & 64) && __builtin_amdgcn_readfirstlane(threadIdx.x) >= 32 * NW) __builtin_amdgcn_s_setprio(1);
     issue(0);
     for (int g = 0; g < nstages; ++g) {
         const bool more = g + 1 < nstages;
-        const bool after_epi = g > 0 && (g - (g / p.nst) * p.nst) == 0;
         if (NBUF == 2 && more) {
             issue(g + 1);
-            if ((p.dbg & 32) && after_epi)
-                asm volatile("s_waitcnt vmcnt(%0)" :: "n"(NBI + 2 * NA * MB) : "memory");
-            else
-                asm volatile("s_waitcnt vmcnt(%0)" :: "n"(NBI) : "memory");
+            asm volatile("s_waitcnt vmcnt(%0)" :: "n"(NBI) : "memory");
         } else {
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         }
