@@ -8,7 +8,8 @@ creation), for every shape: whole and partial tiles, every level, both 16-bit dt
 for the folded decode (box_dfl writes the box rows, head_cls or a class-rows decode the
 scores), including anchor counts that are not a multiple of 8 (96 x 160: A = 315), and for
 the fused C3k2 blocks (c3k2.hip: conv1 -> Residual -> conv2 in one launch), whole and
-partial tiles.
+partial tiles, and for the fused stem (conv.hip stem_fused: the stem and net.p2.0 in one
+launch, the stem output only in LDS), with the engine-dtype and the uint8 input.
 """
 import os
 
@@ -53,6 +54,9 @@ def test_fused_head_equals_per_layer_launches(gpu, variant, dtype, batch, h, w):
     assert "box_dfl" in kinds_f   # decode folded into the box tail (+ head_cls / class-rows decode)
     if variant in ("n", "s"):   # C3k2 blocks with one Residual: net.p2.1 (n, s), net.p3.1 (n)
         assert "c3k2" in kinds_f and "c3k2" not in kinds_p
+        # stem + net.p2.0 (16 -> 32 / 32 -> 64) in one launch
+        assert "net.p1.0+p2.0" in [o["label"] for o in fused.ops(batch, h, w)]
+        assert "net.p1.0+p2.0" not in [o["label"] for o in plain.ops(batch, h, w)]
     if variant == "n":   # s (128) / x (384) cls branches keep the per-layer launches
         assert "head_cls" in kinds_f
         assert len(fused.ops(batch, h, w)) < len(plain.ops(batch, h, w))
@@ -77,3 +81,18 @@ def test_csp_tail_mode_equals_per_layer_launches(gpu, dtype, batch, h, w):
     yt = tail.forward(x).clone()
     yp = plain.forward(x).clone()
     assert torch.equal(yt, yp), (yt.float() - yp.float()).abs().max().item()
+
+
+@pytest.mark.parametrize("variant,dtype,batch,h,w", [("n", torch.float16, 2, 640, 640), ("s", torch.bfloat16, 3, 96, 160)])
+def test_fused_stem_uint8_input(gpu, variant, dtype, batch, h, w):
+    """The fused stem stages the loader's uint8 image with main.py:265-267's `/ 255` exactly
+    like the per-layer stem: uint8 forwards with fusion on and off are bit-identical."""
+    model = make_model(variant)
+    g = torch.Generator().manual_seed(5)
+    x8 = torch.randint(0, 256, (batch, 3, h, w), dtype=torch.uint8, generator=g).to(gpu)
+    fused = _engine(model, dtype, gpu, True)
+    plain = _engine(model, dtype, gpu, False)
+    yf = fused.forward(x8).clone()
+    yp = plain.forward(x8).clone()
+    assert torch.equal(yf, yp), (yf.float() - yp.float()).abs().max().item()
+    assert torch.equal(fused.forward(x8.to(dtype) / 255), yf)

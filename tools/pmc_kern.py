@@ -15,7 +15,7 @@ import sys
 
 def main():
     d = sys.argv[1]
-    pats = [re.compile(p) for p in (sys.argv[2:] or ["head_cls", "csp_fused", "box_dfl", "conv_first", "psa_attention"])]
+    pats = [re.compile(p) for p in (sys.argv[2:] or ["head_cls", "csp_fused", "box_dfl", "conv_first", "stem_fused", "psa_attention"])]
     rows = {}
     for fn in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
         with open(fn) as f:

@@ -22,7 +22,7 @@ import os
 import re
 import sys
 
-FAMILY = {"stem": r"conv_first", "dwconv": r"dwconv", "sppf": r"sppf|maxpool",
+FAMILY = {"stem": r"conv_first|stem_fused", "dwconv": r"dwconv", "sppf": r"sppf|maxpool",
           "attention": r"psa_attention|pe_add", "decode": r"head_decode", "head_cls": r"head_cls", "box_dfl": r"box_dfl", "c3k2": r"csp_fused"}
 
 

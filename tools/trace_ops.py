@@ -14,7 +14,7 @@ import statistics
 import sys
 
 FAMILY = {  # dispatch-name patterns per op class; convs take exactly one dispatch
-    "first": r"conv_first",
+    "first": r"conv_first|stem_fused",
     "dw": r"dwconv",
     "sppf": r"sppf|maxpool",
     "attn": r"psa_attention|pe_add",

@@ -47,6 +47,23 @@ struct FirstConvArgs {
                          //    main.py:265-267's `x.to(dtype) / 255` while staging it
 };
 
+// Stem + net.p2.0 fused (nets/nn.py:160-163): the stem output stays in LDS.
+struct Stem2Args {
+    const void* const* io;   // io[0] = x (NCHW, 3 channels; uint8 when in_u8)
+    int H, W, Hs, Ws, Ho, Wo, B;
+    const float* w1;         // stem weights [27][c1p] fp32 (k = ci*9 + kh*3 + kw)
+    const float* b1;         // stem bias [c1p]
+    int c1, c1p, c2;         // stem couts, its padded stride in w1, p2.0 couts
+    const void* prm;         // p2.0 fragments (c2/32 tiles x 9*c1/16 steps x 1 KB, MFMA lane order) + fp32 bias
+    int prm_bias;            // byte offset of the bias in prm
+    void* out; int ldo;      // p2.0 output view
+    int in_u8;
+    int ntw, nth;            // tiles per row / per column (stem2_tiles)
+};
+bool stem2_ok(int c1, int c2);
+void stem2_tiles(int Ho, int Wo, int& ntw, int& nth);
+int launch_stem2(int dtype, const Stem2Args& a, hipStream_t s);
+
 // Depthwise 3x3 stride-1 conv on an NHWC view.
 struct DwArgs {
     const void* in; int ldi;

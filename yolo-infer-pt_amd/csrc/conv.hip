@@ -597,6 +597,209 @@ int launch_first_t(const FirstConvArgs& a, int B, hipStream_t s) {
     return a.in_u8 ? launch_first_tu<T, uint8_t>(a, B, s) : launch_first_tu<T, T>(a, B, s);
 }
 
+// ---------------------------------------------------------------------------
+// Stem + net.p2.0 in one launch (nets/nn.py:160-163: Conv(3, w1, 3, 2) -> Conv(w1, w2,
+// 3, 2), both SiLU): the stem's output, 2x the p2.0 output in each direction plus a
+// 1-pixel halo, lives only in LDS, so its HBM write and re-read (105 MB each at v11_n
+// b32 640^2) disappear.
+// A workgroup (4 waves) owns S2_TH x S2_TW p2.0 outputs of one image:
+//   1. the 3 x (4 S2_TH + 3) x (4 S2_TW + 3) input window -> LDS (8-aligned chunks,
+//      wholly inside the image or zero, exactly as conv_first_tile stages it);
+//   2. the (2 S2_TH + 1) x (2 S2_TW + 1) stem pixels: conv_first_tile's arithmetic (k =
+//      ci*9 + kh*3 + kw on v_mfma_f32_16x16x32, bias, SiLU, one rounding), stored NHWC
+//      in LDS; pixels outside the stem map are p2.0's zero padding and stored as 0;
+//   3. p2.0 on v_mfma_f32_32x32x16 in conv_mx's canonical K order (for 16-channel block:
+//      for tap: one step), bias, SiLU, one rounding (mx_epi) -> HBM.
+// Output is bit-identical to conv_first_tile followed by conv_mx.
+constexpr int S2_TH = 4, S2_TW = 32, S2_NT = 256;
+constexpr int S2_SR = 2 * S2_TH + 1, S2_SC = 2 * S2_TW + 1;   // stem region (rows, cols)
+constexpr int S2_IR = 2 * S2_SR + 1;                          // input rows per channel
+constexpr int S2_ICH = (4 * S2_TW + 16) / 8;                  // 8-element chunks per input row
+constexpr int S2_ISEG = 8 * S2_ICH;                           // staged columns (from 4 wo0 - 8)
+constexpr int S2_NPX = S2_SR * S2_SC;                         // stem pixels per tile
+typedef __attribute__((ext_vector_type(16))) float f32x16_s;
+
+template <typename T>
+__device__ __forceinline__ f32x16_s s2_mfma(const uint4& a, const uint4& b, const f32x16_s& c) {
+    if constexpr (std::is_same<T, __bf16>::value)
+        return __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, a), __builtin_bit_cast(bf16x8, b), c, 0,
+                                                       0, 0);
+    else
+        return __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(f16x8, a), __builtin_bit_cast(f16x8, b), c, 0, 0,
+                                                      0);
+}
+template <typename T>
+__device__ __forceinline__ unsigned s2_pack2(float a, float b) {
+    typedef __attribute__((ext_vector_type(2))) float f2;
+    typedef __attribute__((ext_vector_type(2))) T t2;
+    return __builtin_bit_cast(unsigned, __builtin_convertvector(f2{a, b}, t2));
+}
+
+template <typename T, typename U, int C1, int C2>
+__global__ __launch_bounds__(S2_NT) void stem_fused(const Stem2Args p) {
+    static_assert(sizeof(T) == 2, "16-bit path");
+    constexpr int PS = 2 * C1 + 1;   // 16-B chunks per stored stem pixel (+1: 2-way banks on stride-2 reads)
+    constexpr int KS = 9 * C1;       // p2.0 K steps
+    constexpr int RPW = C2;          // output rows per wave (S2_TH rows x C2 cout tiles over 4 waves)
+    static_assert(S2_TH * C2 == 4 * RPW, "4 waves");
+    __shared__ __attribute__((aligned(16))) T patch[3 * S2_IR][S2_ISEG];
+    __shared__ uint4 sout[S2_NPX * PS];
+    const int tx = blockIdx.x % p.ntw, ty = blockIdx.x / p.ntw, n = blockIdx.y;
+    const int ho0 = ty * S2_TH, wo0 = tx * S2_TW;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int h = lane >> 5, l32 = lane & 31;
+
+    // p2.0 weight fragments of this wave's cout tile: issued first, consumed last
+    const int a2 = wave % C2;
+    uint4 af[KS];
+    {
+        const uint4* w2 = reinterpret_cast<const uint4*>(p.prm) + (size_t)a2 * KS * 64 + lane;
+#pragma unroll
+        for (int s = 0; s < KS; ++s) af[s] = w2[s * 64];
+    }
+
+    // 1. input window: rows 4 ho0 - 3 .., columns 4 wo0 - 8 .. (chunk-aligned)
+    const U* x = reinterpret_cast<const U*>(p.io[0]);
+    const int ir0 = 4 * ho0 - 3, ca = 4 * wo0 - 8;
+    const long long plane = (long long)p.H * p.W;
+    {
+        constexpr int TOT = 3 * S2_IR * S2_ICH;
+        constexpr int NCH = (TOT + S2_NT - 1) / S2_NT;
+        using Raw = typename std::conditional<sizeof(U) == 1, uint2, uint4>::type;
+        Raw raw[NCH];
+        bool ok[NCH];
+#pragma unroll
+        for (int u = 0; u < NCH; ++u) {
+            const int c = min(tid + u * S2_NT, TOT - 1);
+            const int seg = c / S2_ICH, ch = c - seg * S2_ICH;
+            const int ci = seg / S2_IR, rr = seg - ci * S2_IR;
+            const int hi = ir0 + rr, col = ca + 8 * ch;
+            ok[u] = hi >= 0 && hi < p.H && col >= 0 && col + 8 <= p.W;
+            const int hc = min(max(hi, 0), p.H - 1), cc = min(max(col, 0), p.W - 8);
+            raw[u] = *reinterpret_cast<const Raw*>(x + ((long long)n * 3 + ci) * plane + (long long)hc * p.W + cc);
+        }
+#pragma unroll
+        for (int u = 0; u < NCH; ++u) {
+            const int c = tid + u * S2_NT;
+            if (c >= TOT) continue;
+            const int seg = c / S2_ICH, ch = c - seg * S2_ICH;
+            uint4 v;
+            if constexpr (sizeof(U) == 1) {
+                float f[8];
+#pragma unroll
+                for (int e = 0; e < 8; ++e)
+                    f[e] = stem_in<uint8_t, T>((uint8_t)(((e < 4 ? raw[u].x : raw[u].y) >> (8 * (e & 3))) & 255u));
+                v = f_to_chunk<T>(f).v[0];
+            } else {
+                v = raw[u];
+            }
+            *reinterpret_cast<uint4*>(&patch[seg][ch * 8]) = ok[u] ? v : make_uint4(0, 0, 0, 0);
+        }
+    }
+    // stem weights / biases (conv_first_tile's fragments)
+    const int fr = lane & 15, g = lane >> 4;
+    uint4 wf[C1];
+    float bv[C1][4];
+#pragma unroll
+    for (int i = 0; i < C1; ++i) {
+        float f[8];
+        const int co = 16 * i + fr;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const int k = 8 * g + j;
+            f[j] = k < 27 ? p.w1[k * p.c1p + co] : 0.f;
+        }
+        wf[i] = f_to_chunk<T>(f).v[0];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) bv[i][r] = p.b1[16 * i + 4 * g + r];
+    }
+    int koff[8];
+    bool kok[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        const int k = 8 * g + j;
+        const int ci = k / 9, kh = (k - ci * 9) / 3, kw = k - ci * 9 - kh * 3;
+        kok[j] = k < 27;
+        koff[j] = kok[j] ? (ci * S2_IR + kh) * S2_ISEG + kw : 0;
+    }
+    __syncthreads();
+
+    // 2. stem pixels of the region: stem row 2 ho0 - 1 + sr, col 2 wo0 - 1 + sc
+    {
+        const T* pbase = &patch[0][0];
+        constexpr int NG = (S2_NPX + 15) / 16;
+        for (int gi = wave; gi < NG; gi += S2_NT / 64) {
+            const int q = min(gi * 16 + fr, S2_NPX - 1);
+            const int sr = q / S2_SC, sc = q - sr * S2_SC;
+            const int b0 = 2 * sr * S2_ISEG + 2 * sc + 5;
+            T xv[8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) xv[j] = kok[j] ? pbase[b0 + koff[j]] : fromf<T>(0.f);
+            const uint4 xf = *reinterpret_cast<const uint4*>(xv);
+            const int gs = 2 * ho0 - 1 + sr, gc = 2 * wo0 - 1 + sc;
+            const bool live = gs >= 0 && gs < p.Hs && gc >= 0 && gc < p.Ws;
+#pragma unroll
+            for (int i = 0; i < C1; ++i) {
+                f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+                Mma<T>::step(acc, &wf[i], &xf);
+                unsigned u[4];
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    float v = acc[r] + bv[i][r];
+                    v = silu<T>(v);
+                    u[r] = live ? (unsigned short)__builtin_bit_cast(short, fromf<T>(v)) : 0u;
+                }
+                if (gi * 16 + fr < S2_NPX)
+                    *reinterpret_cast<uint2*>(reinterpret_cast<char*>(sout) + q * PS * 16 + (16 * i + 4 * g) * 2) =
+                        make_uint2(u[0] | (u[1] << 16), u[2] | (u[3] << 16));
+            }
+        }
+    }
+    __syncthreads();
+
+    // 3. p2.0: wave -> cout tile a2, output rows r = wave / C2 + k * (4 / C2), 32 px each
+    {
+        const float* bias2 = reinterpret_cast<const float*>(reinterpret_cast<const char*>(p.prm) + p.prm_bias);
+        const int co = 32 * a2 + 16 * h;
+        float b2[16];
+#pragma unroll
+        for (int i = 0; i < 16; ++i) b2[i] = bias2[co + i];
+        T* out = reinterpret_cast<T*>(p.out);
+#pragma unroll
+        for (int k = 0; k < RPW; ++k) {
+            const int r = wave / C2 + k * (4 / C2);
+            f32x16_s acc;
+#pragma unroll
+            for (int e = 0; e < 16; ++e) acc[e] = 0.f;
+#pragma unroll
+            for (int s = 0; s < KS; ++s) {
+                const int cb = s / 9, tap = s - 9 * cb, kh = tap / 3, kw = tap - 3 * kh;
+                const int q = (2 * r + kh) * S2_SC + 2 * l32 + kw;
+                acc = s2_mfma<T>(af[s], sout[q * PS + 2 * cb + h], acc);
+            }
+            const int ho = ho0 + r, wo = wo0 + l32;
+            if (ho < p.Ho && wo < p.Wo) {
+                unsigned w[8];
+#pragma unroll
+                for (int e = 0; e < 16; e += 2) w[e >> 1] = s2_pack2<T>(silu<T>(acc[e] + b2[e]), silu<T>(acc[e + 1] + b2[e + 1]));
+                uint4* d = reinterpret_cast<uint4*>(out + (((long long)n * p.Ho + ho) * p.Wo + wo) * p.ldo + co);
+                d[0] = make_uint4(w[0], w[1], w[2], w[3]);
+                d[1] = make_uint4(w[4], w[5], w[6], w[7]);
+            }
+        }
+    }
+}
+
+template <typename T, typename U>
+int launch_stem2_tu(const Stem2Args& a, hipStream_t s) {
+    const dim3 grid((unsigned)(a.ntw * a.nth), (unsigned)a.B);
+    if (a.c1 == 16 && a.c2 == 32) hipLaunchKernelGGL((stem_fused<T, U, 1, 1>), grid, dim3(S2_NT), 0, s, a);
+    else if (a.c1 == 32 && a.c2 == 64) hipLaunchKernelGGL((stem_fused<T, U, 2, 2>), grid, dim3(S2_NT), 0, s, a);
+    else return (int)hipErrorInvalidValue;
+    return (int)hipGetLastError();
+}
+
 // Depthwise 3x3, stride 1, pad 1 (nn.py:248,250). One thread = 8 channels x DW_ROWS
 // vertically adjacent output pixels: the DW_ROWS + 2 input rows it needs are
 // loaded once (no per-tap re-read of the shared rows), all loads are issued before
@@ -772,6 +975,21 @@ int launch_first_conv(int dtype, const FirstConvArgs& a, int B, hipStream_t s) {
         case F32: return launch_first_t<float>(a, B, s);
         case F16: return launch_first_t<_Float16>(a, B, s);
         case BF16: return launch_first_t<__bf16>(a, B, s);
+    }
+    return (int)hipErrorInvalidValue;
+}
+
+bool stem2_ok(int c1, int c2) { return (c1 == 16 && c2 == 32) || (c1 == 32 && c2 == 64); }
+void stem2_tiles(int Ho, int Wo, int& ntw, int& nth) {
+    ntw = (Wo + S2_TW - 1) / S2_TW;
+    nth = (Ho + S2_TH - 1) / S2_TH;
+}
+
+int launch_stem2(int dtype, const Stem2Args& a, hipStream_t s) {
+    if (!stem2_ok(a.c1, a.c2) || a.W % 8 || a.ldo % 8) return (int)hipErrorInvalidValue;
+    switch (dtype) {
+        case F16: return a.in_u8 ? launch_stem2_tu<_Float16, uint8_t>(a, s) : launch_stem2_tu<_Float16, _Float16>(a, s);
+        case BF16: return a.in_u8 ? launch_stem2_tu<__bf16, uint8_t>(a, s) : launch_stem2_tu<__bf16, __bf16>(a, s);
     }
     return (int)hipErrorInvalidValue;
 }

@@ -89,7 +89,7 @@ static uint16_t f2h(float f) {
 
 // ---------------------------------------------------------------- graph model
 enum ConvKind { CK_DENSE = 0, CK_FIRST = 1, CK_DW = 2, CK_PE = 3 };
-enum OpKind { OP_FIRST, OP_CONV, OP_DW, OP_SPPF, OP_ATTN, OP_DECODE, OP_HEADCLS, OP_BOXDFL, OP_CSP };
+enum OpKind { OP_FIRST, OP_CONV, OP_DW, OP_SPPF, OP_ATTN, OP_DECODE, OP_HEADCLS, OP_BOXDFL, OP_CSP, OP_STEM2 };
 enum OpClass { CL_CONV3 = 0, CL_CONV1 = 1, CL_FIRST = 2, CL_DW = 3, CL_SPPF = 4, CL_ATTN = 5, CL_DECODE = 6,
                CL_HEADCLS = 7, CL_BOXDFL = 8, CL_CSP = 9, CL_N = 10 };
 
@@ -134,6 +134,7 @@ struct Op {
     int dlo = 0;
     bool dbox = true;
     // OP_CSP: conv1, res_m.0.conv1, res_m.0.conv2, conv2 of a fused C3k2 block (in[0] -> out)
+    // OP_STEM2: cs[0] = net.p2.0 (conv = the stem)
     int cs[4] = {-1, -1, -1, -1};
     std::string label;
 };
@@ -363,8 +364,19 @@ struct Net {
         const bool c0 = var.csp[0] != 0, c1 = var.csp[1] != 0;
         const int nc = var.num_classes;
         // ---- DarkNet (nn.py:151-189)
-        const int t1 = tensor(1, w[1]);
-        {
+        const int t2 = tensor(2, w[2]);
+        if (fuse_stem(w[0], w[1], w[2])) {
+            // stem + net.p2.0 in one launch: the stem output never reaches HBM
+            Op op;
+            op.kind = OP_STEM2;
+            op.conv = new_conv("net.p1.0", CK_FIRST, w[0], w[1], 3, 2, 1, 0, ACT_SILU);
+            op.cs[0] = new_dense_conv("net.p2.0", w[1], w[2], 3, 0, ACT_SILU);
+            convs[op.cs[0]].stride = 2;
+            op.out = full(t2, w[2]);
+            op.label = "net.p1.0+p2.0";
+            ops.push_back(op);
+        } else {
+            const int t1 = tensor(1, w[1]);
             const int ci = new_conv("net.p1.0", CK_FIRST, w[0], w[1], 3, 2, 1, 0, ACT_SILU);
             Op op;
             op.kind = OP_FIRST;
@@ -372,9 +384,8 @@ struct Net {
             op.out = full(t1, w[1]);
             op.label = "net.p1.0";
             ops.push_back(op);
+            conv3("net.p2.0", full(t1, w[1]), w[1], w[2], 2, ACT_SILU, full(t2, w[2]));
         }
-        const int t2 = tensor(2, w[2]);
-        conv3("net.p2.0", full(t1, w[1]), w[1], w[2], 2, ACT_SILU, full(t2, w[2]));
         const int t2b = tensor(2, w[3]);
         csp("net.p2.1", {Seg{full(t2, w[2]), 0}}, {w[2]}, w[3], d[0], c0, 4, full(t2b, w[3]), 2);
         const int t3 = tensor(3, w[3]);
@@ -488,6 +499,44 @@ struct Net {
         const int ci = new_conv(name, CK_DENSE, cin, cout, k, 1, 1, has_bias, act);
         convs[ci].segs.push_back({cin, round_up(cin, 8)});
         return ci;
+    }
+    // the stem and net.p2.0 run fused (conv.hip stem_fused) on 16-bit handles for the
+    // instantiated widths (v11_n 16 -> 32, v11_s 32 -> 64)
+    bool fuse_stem(int c0, int c1, int c2) const {
+        const char* e = getenv("YH_FUSE");
+        if (dtype == F32 || (e && atoi(e) == 0)) return false;
+        const char* e2 = getenv("YH_FUSE_STEM");
+        if (e2 && atoi(e2) == 0) return false;
+        return c0 == 3 && stem2_ok(c1, c2);
+    }
+    // packed p2.0 parameters of the fused stem: fragments (tile a, step k = cb*9 + tap,
+    // lane, j) in MFMA lane order with conv_mx's row permutation, then the fp32 bias
+    const void* stem2_params(const Op& op, int& bias_off) {
+        ConvDesc& d = convs[op.cs[0]];
+        const int nt = d.cout / 32, nk = 9 * (d.cin / 16);
+        bias_off = nt * nk * 1024;
+        auto it = d.mx_w.find("stem2");
+        if (it != d.mx_w.end()) return it->second;
+        require(d.loaded, "weights of " + d.name + " not loaded", YH_ESTATE);
+        std::vector<uint8_t> img((size_t)bias_off + (size_t)d.cout * 4, 0);
+        uint16_t* dst = reinterpret_cast<uint16_t*>(img.data());
+        for (int a = 0; a < nt; ++a)
+            for (int k = 0; k < nk; ++k)
+                for (int lane = 0; lane < 64; ++lane)
+                    for (int j = 0; j < 8; ++j) {
+                        const int R = lane & 31, hh = lane >> 5;
+                        const int co = 32 * a + 16 * ((R >> 2) & 1) + (R & 3) + 4 * (R >> 3);
+                        const int cb = k / 9, tap = k - cb * 9, ch = 16 * cb + 8 * hh + j;
+                        const float v = d.wf[((size_t)co * d.cin + ch) * 9 + tap];
+                        dst[((size_t)(a * nk + k) * 64 + lane) * 8 + j] = dtype == BF16 ? f2bf(v) : f2h(v);
+                    }
+        float* bd = reinterpret_cast<float*>(img.data() + bias_off);
+        for (int i = 0; i < d.cout; ++i) bd[i] = d.bf[i];
+        void* dev = nullptr;
+        HIPCHECK(hipMalloc(&dev, img.size()));
+        HIPCHECK(hipMemcpy(dev, img.data(), img.size(), hipMemcpyHostToDevice));
+        d.mx_w.emplace("stem2", dev);
+        return dev;
     }
     // a C3k2 block with one Residual runs fused (c3k2.hip) on 16-bit handles when its input
     // is one plain view of 16-channel blocks and (Cin, c, cout) has an instantiated kernel
@@ -1200,6 +1249,22 @@ struct Net {
                 break;
             }
             case OP_BOXDFL: rc = launch_box_dfl(dtype, box_dfl_args(op, B, H, W), s); break;
+            case OP_STEM2: {
+                const ConvDesc& d = convs[op.conv];
+                Stem2Args a{};
+                a.io = (const void* const*)io_dev;
+                a.H = H; a.W = W; a.Hs = H >> 1; a.Ws = W >> 1; a.Ho = H >> 2; a.Wo = W >> 2; a.B = B;
+                a.w1 = (const float*)d.w_dev;
+                a.b1 = d.b_dev;
+                a.c1 = d.cout; a.c1p = d.cout_p; a.c2 = convs[op.cs[0]].cout;
+                a.prm = stem2_params(op, a.prm_bias);
+                a.out = ptr(op.out);
+                a.ldo = ldc(op.out);
+                a.in_u8 = in_u8;
+                stem2_tiles(a.Ho, a.Wo, a.ntw, a.nth);
+                rc = launch_stem2(dtype, a, s);
+                break;
+            }
             case OP_CSP: {
                 CspArgs a{};
                 const View& xv = op.in[0].v;
@@ -1354,6 +1419,7 @@ struct Net {
             case OP_HEADCLS: return CL_HEADCLS;
             case OP_BOXDFL: return CL_BOXDFL;
             case OP_CSP: return CL_CSP;
+            case OP_STEM2: return CL_FIRST;
         }
         return CL_CONV1;
     }
@@ -1431,6 +1497,16 @@ struct Net {
                     bytes = 2.0 * A * var.num_classes * es;
                     flops = A * var.num_classes * 4.0;
                 }
+                break;
+            }
+            case OP_STEM2: {
+                // the image read once, p2.0's output written once, both weights once
+                const ConvDesc& d = convs[op.conv];
+                const ConvDesc& d2 = convs[op.cs[0]];
+                const double s1 = px(1), o2 = px(2);
+                bytes = (double)B * 3 * H * W * (in_u8 ? 1 : es) + o2 * d2.cout * es + d.cout * 27.0 * 4 +
+                        (double)d2.cout * d2.cin * 9 * es;
+                flops = 2.0 * s1 * d.cout * 27 + 2.0 * o2 * d2.cout * d2.cin * 9;
                 break;
             }
             case OP_CSP: {
