@@ -1004,7 +1004,10 @@ struct Net {
 
     // Pick the conv_mx plan of every dense conv for this shape: one plain forward with
     // each layer's default plan (realistic activations in the workspace), then every
-    // candidate plan of every layer timed over 3 launches after a warm-up launch. The
+    // candidate plan of every layer timed over 3 launches after a warm-up launch, each
+    // right after the forward's preceding op (in situ; the input's cache state of the
+    // forward: back-to-back launches of one layer favoured plans that re-read a
+    // MALL-resident input, e.g. net.p3.0's 32-B-per-stage plan at 2x HBM traffic). The
     // candidates are bit-identical (one reduction order), so the choice only changes
     // speed. Runs outside any graph capture; the next forward recomputes everything.
     void ensure_tuned(int B, int H, int W, hipStream_t s) {
@@ -1046,6 +1049,8 @@ struct Net {
         cur_kern = &slot;
         if (forced >= 0) return;
         run_ops(B, H, W, s);
+        // YH_TUNE_INSITU=0 (experiments): time candidates back to back instead
+        static const bool insitu = [] { const char* e = getenv("YH_TUNE_INSITU"); return !e || atoi(e) != 0; }();
         hipEvent_t e0, e1;
         HIPCHECK(hipEventCreate(&e0));
         HIPCHECK(hipEventCreate(&e1));
@@ -1054,13 +1059,29 @@ struct Net {
             float best = 1e30f;
             for (const MxPlan& pl : cands[i]) {
                 int rc = launch_mx_op(ops[i], pl, B, H, W, s);
-                HIPCHECK(hipEventRecord(e0, s));
-                for (int r = 0; r < 3 && rc == 0; ++r) rc = launch_mx_op(ops[i], pl, B, H, W, s);
-                HIPCHECK(hipEventRecord(e1, s));
-                HIPCHECK(hipEventSynchronize(e1));
-                if (rc != 0) throw Fail(YH_EHIP, "tuning launch of " + ops[i].label + " failed");
                 float ms = 0.f;
-                HIPCHECK(hipEventElapsedTime(&ms, e0, e1));
+                if (insitu && i > 0) {
+                    // in situ: each timed launch right after the op that precedes it in the
+                    // forward, so the input's cache state (just written, L2 / MALL warm, the
+                    // layer's other operands cold) is the forward's, not a back-to-back loop's
+                    for (int r = 0; r < 3 && rc == 0; ++r) {
+                        launch_op(i - 1, B, H, W, s);
+                        HIPCHECK(hipEventRecord(e0, s));
+                        rc = launch_mx_op(ops[i], pl, B, H, W, s);
+                        HIPCHECK(hipEventRecord(e1, s));
+                        HIPCHECK(hipEventSynchronize(e1));
+                        float t = 0.f;
+                        HIPCHECK(hipEventElapsedTime(&t, e0, e1));
+                        ms += t;
+                    }
+                } else {
+                    HIPCHECK(hipEventRecord(e0, s));
+                    for (int r = 0; r < 3 && rc == 0; ++r) rc = launch_mx_op(ops[i], pl, B, H, W, s);
+                    HIPCHECK(hipEventRecord(e1, s));
+                    HIPCHECK(hipEventSynchronize(e1));
+                    HIPCHECK(hipEventElapsedTime(&ms, e0, e1));
+                }
+                if (rc != 0) throw Fail(YH_EHIP, "tuning launch of " + ops[i].label + " failed");
                 if (tune_log)
                     fprintf(stderr, "[yh tune] %-36s %-40s %8.2f us\n", ops[i].label.c_str(), mx_name(pl).c_str(),
                             ms * 1e3f / 3);
