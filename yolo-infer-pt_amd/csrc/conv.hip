@@ -614,8 +614,8 @@ int launch_first_t(const FirstConvArgs& a, int B, hipStream_t s) {
 constexpr int S2_TH = 4, S2_TW = 32, S2_NT = 256;
 constexpr int S2_SR = 2 * S2_TH + 1, S2_SC = 2 * S2_TW + 1;   // stem region (rows, cols)
 constexpr int S2_IR = 2 * S2_SR + 1;                          // input rows per channel
-constexpr int S2_ICH = (4 * S2_TW + 16) / 8;                  // 8-element chunks per input row
-constexpr int S2_ISEG = 8 * S2_ICH;                           // staged columns (from 4 wo0 - 8)
+constexpr int S2_ICH = (4 * S2_TW + 32) / 8;                  // 8-element chunks per input row
+constexpr int S2_ISEG = 8 * S2_ICH;                           // staged columns (from 4 wo0 - 32: 64-B aligned)
 constexpr int S2_NPX = S2_SR * S2_SC;                         // stem pixels per tile
 typedef __attribute__((ext_vector_type(16))) float f32x16_s;
 
@@ -659,9 +659,10 @@ __global__ __launch_bounds__(S2_NT) void stem_fused(const Stem2Args p) {
         for (int s = 0; s < KS; ++s) af[s] = w2[s * 64];
     }
 
-    // 1. input window: rows 4 ho0 - 3 .., columns 4 wo0 - 8 .. (chunk-aligned)
+    // 1. input window: rows 4 ho0 - 3 .., columns 4 wo0 - 32 .. (64-B aligned rows for 16-bit
+    //    input: whole 64-B sectors, no partial-sector fetches at the row ends)
     const U* x = reinterpret_cast<const U*>(p.io[0]);
-    const int ir0 = 4 * ho0 - 3, ca = 4 * wo0 - 8;
+    const int ir0 = 4 * ho0 - 3, ca = 4 * wo0 - 32;
     const long long plane = (long long)p.H * p.W;
     {
         constexpr int TOT = 3 * S2_IR * S2_ICH;
@@ -732,7 +733,7 @@ __global__ __launch_bounds__(S2_NT) void stem_fused(const Stem2Args p) {
         for (int gi = wave; gi < NG; gi += S2_NT / 64) {
             const int q = min(gi * 16 + fr, S2_NPX - 1);
             const int sr = q / S2_SC, sc = q - sr * S2_SC;
-            const int b0 = 2 * sr * S2_ISEG + 2 * sc + 5;
+            const int b0 = 2 * sr * S2_ISEG + 2 * sc + 29;
             T xv[8];
 #pragma unroll
             for (int j = 0; j < 8; ++j) xv[j] = kok[j] ? pbase[b0 + koff[j]] : fromf<T>(0.f);
