@@ -1002,9 +1002,15 @@ std::vector<MxPlan> mx_candidates(const MxShape& sh, int num_cus) {
     } else if (sh.ks == 3) {
         // stride 2: a 4x8 wave tile (9x17 patch) double-buffered, or an 8x8 tile (17x17)
         // single-buffered; 32-cout slices for weights too large to keep whole
+        // 16-channel stages read 32 B of each input pixel per stage: on an input far beyond
+        // L2 (net.p3.0: 105 MB) that costs 2x its bytes in HBM traffic (PMC), and in-situ
+        // timing does not separate the two reliably, so only 32-channel stages there
+        const bool big_in = (double)sh.B * sh.Hi * sh.Wi * sh.cin * 2.0 > 64e6 && sh.cin >= 64;
         if (narrow) { addr(1, 1, 1, 5); addr(1, 2, 1, 10, 1); }
-        else { addr(2, 1, 1, 5); addr(2, 2, 1, 10, 1); addr(1, 1, 1, 5); addr(1, 2, 1, 10, 1);
-               addr(2, 1, 2, 10, 2, 4); addr(1, 1, 2, 10, 2, 4); }
+        else {
+            if (!big_in) { addr(2, 1, 1, 5); addr(2, 2, 1, 10, 1); addr(1, 1, 1, 5); addr(1, 2, 1, 10, 1); }
+            addr(2, 1, 2, 10, 2, 4); addr(1, 1, 2, 10, 2, 4);
+        }
     } else {
         if (narrow) { addr(1, 2, 1, 2); addr(1, 2, 2, 4); addr(1, 2, 4, 8); addr(1, 4, 1, 4); addr(1, 4, 2, 8);
                       addr(1, 1, 2, 2); addr(1, 1, 4, 4); }
