@@ -297,12 +297,14 @@ __device__ __forceinline__ bool iou_fast(float ax1, float ay1, float ax2, float 
     const float xx2 = fminf(ax2, bx2), yy2 = fminf(ay2, by2);
     const float w = fmaxf(0.0f, xx2 - xx1), h = fmaxf(0.0f, yy2 - yy1);
     const float inter = w * h;
+    // most pairs do not intersect (every class is offset by c * max_wh): they skip the fp64
+    // test (wave-uniform when no lane of the wave intersects)
+    if (!(inter > 0.0f)) return false;
     const float uni = aa + ba - inter;
     const double lhs = (double)inter, rhs = th.m * (double)uni;
-    const bool pos = inter > 0.0f;
     const bool good = (uni > 0.0f) & (uni < 3.0e38f) & (inter < 3.0e38f);
-    slow |= pos & !good;
-    return pos & good & ((lhs > rhs) | ((lhs == rhs) & th.tie_up));
+    slow |= !good;
+    return good & ((lhs > rhs) | ((lhs == rhs) & th.tie_up));
 }
 
 // Greedy NMS over the first `want` keys of the sorted batch, in sub-batches of SB
