@@ -642,7 +642,8 @@ __global__ __launch_bounds__(S2_NT) void stem_fused(const Stem2Args p) {
     constexpr int KS = 9 * C1;       // p2.0 K steps
     constexpr int RPW = C2;          // output rows per wave (S2_TH rows x C2 cout tiles over 4 waves)
     static_assert(S2_TH * C2 == 4 * RPW, "4 waves");
-    __shared__ __attribute__((aligned(16))) T patch[3 * S2_IR][S2_ISEG];
+    // + one zero row: the padded K values (k >= 27) read it instead of branching
+    __shared__ __attribute__((aligned(16))) T patch[3 * S2_IR + 1][S2_ISEG];
     __shared__ uint4 sout[S2_NPX * PS];
     const int tx = blockIdx.x % p.ntw, ty = blockIdx.x / p.ntw, n = blockIdx.y;
     const int ho0 = ty * S2_TH, wo0 = tx * S2_TW;
@@ -698,6 +699,7 @@ __global__ __launch_bounds__(S2_NT) void stem_fused(const Stem2Args p) {
             *reinterpret_cast<uint4*>(&patch[seg][ch * 8]) = ok[u] ? v : make_uint4(0, 0, 0, 0);
         }
     }
+    if (tid < S2_ISEG / 8) *reinterpret_cast<uint4*>(&patch[3 * S2_IR][tid * 8]) = make_uint4(0, 0, 0, 0);
     // stem weights / biases (conv_first_tile's fragments)
     const int fr = lane & 15, g = lane >> 4;
     uint4 wf[C1];
@@ -726,17 +728,22 @@ __global__ __launch_bounds__(S2_NT) void stem_fused(const Stem2Args p) {
     }
     __syncthreads();
 
-    // 2. stem pixels of the region: stem row 2 ho0 - 1 + sr, col 2 wo0 - 1 + sc
+    // 2. stem pixels of the region: stem row 2 ho0 - 1 + sr, col 2 wo0 - 1 + sc; every group of
+    //    the wave unrolled (the LDS gathers of later groups overlap earlier groups' epilogues)
     {
         const T* pbase = &patch[0][0];
-        constexpr int NG = (S2_NPX + 15) / 16;
-        for (int gi = wave; gi < NG; gi += S2_NT / 64) {
+        constexpr int NG = (S2_NPX + 15) / 16, NIT = (NG + S2_NT / 64 - 1) / (S2_NT / 64);
+        constexpr int ZIDX = 3 * S2_IR * S2_ISEG;   // the zero row
+#pragma unroll
+        for (int it = 0; it < NIT; ++it) {
+            const int gi = wave + it * (S2_NT / 64);
+            if (gi >= NG) break;
             const int q = min(gi * 16 + fr, S2_NPX - 1);
             const int sr = q / S2_SC, sc = q - sr * S2_SC;
             const int b0 = 2 * sr * S2_ISEG + 2 * sc + 29;
             T xv[8];
 #pragma unroll
-            for (int j = 0; j < 8; ++j) xv[j] = kok[j] ? pbase[b0 + koff[j]] : fromf<T>(0.f);
+            for (int j = 0; j < 8; ++j) xv[j] = pbase[kok[j] ? b0 + koff[j] : ZIDX];
             const uint4 xf = *reinterpret_cast<const uint4*>(xv);
             const int gs = 2 * ho0 - 1 + sr, gc = 2 * wo0 - 1 + sc;
             const bool live = gs >= 0 && gs < p.Hs && gc >= 0 && gc < p.Ws;
