@@ -11,7 +11,8 @@ cv2.resize's INTER_LINEAR for 8-bit images, vectorised here with numpy from
 OpenCV's published algorithm (imgproc/resize.cpp): 11-bit coefficients from the
 float source coordinate, an exact integer horizontal pass, and the vertical pass
 as its SIMD kernel rounds (VResizeLinearVec_32s8u: (S >> 4) * beta >> 16, + 2,
->> 2); an exact 2x downscale is routed to INTER_AREA's fast path. cv2 is absent
+>> 2) over the bytes its 128-bit vector loops cover, and the scalar FixedPtCast
+((S0 b0 + S1 b1 + 2^21) >> 22) on the row's tail bytes (see `vtail`); an exact 2x downscale is routed to INTER_AREA's fast path. cv2 is absent
 from this image and no fixture of cv2 output exists in the reference: PARITY
 UNPINNED against cv2 itself. The kernels are pinned to this restatement, and this
 restatement to torch's half-pixel bilinear resize within one grey level.
@@ -40,6 +41,16 @@ def _axis(n_dst, n_src, clamp):
     return np.clip(s, 0, n_src - 1), np.clip(s + 1, 0, n_src - 1), a0, a1
 
 
+def vtail(width):
+    """First byte of a resized row that OpenCV's vertical pass computes in its scalar loop:
+    VResizeLinearVec_32s8u steps 16 bytes while x <= width - 16, then 8 bytes while
+    x < width - 8 (128-bit universal intrinsics); the rest is scalar."""
+    x = ((width - 16) // 16 + 1) * 16 if width >= 16 else 0
+    if x < width - 8:
+        x += 8
+    return x
+
+
 def resize_linear(img, nh, nw):
     """cv2.resize(img, (nw, nh), interpolation=INTER_LINEAR) for an (h, w, 3) uint8 image."""
     h, w = img.shape[:2]
@@ -54,7 +65,10 @@ def resize_linear(img, nh, nw):
     horiz = src[:, xs0] * xa0[None, :, None] + src[:, xs1] * xa1[None, :, None]   # (h, nw, 3)
     t0 = ((horiz[ys0] >> 4) * ya0[:, None, None]) >> 16
     t1 = ((horiz[ys1] >> 4) * ya1[:, None, None]) >> 16
-    return np.clip((t0 + t1 + 2) >> 2, 0, 255).astype(np.uint8)
+    vec = (t0 + t1 + 2) >> 2
+    sca = (horiz[ys0] * ya0[:, None, None] + horiz[ys1] * ya1[:, None, None] + (1 << 21)) >> 22
+    byte = (np.arange(nw)[:, None] * 3 + np.arange(3)[None, :])[None]   # byte index within the row
+    return np.clip(np.where(byte < vtail(3 * nw), vec, sca), 0, 255).astype(np.uint8)
 
 
 def letterbox(img, size):

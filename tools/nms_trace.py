@@ -1,4 +1,7 @@
-"""Phase timing of the NMS kernels on a real v11_n bf16 head output (debug hook yh_debug_nms_trace)."""
+"""Phase timing of the NMS kernels on a real v11_n bf16 head output (debug hook yh_debug_nms_trace).
+
+Needs the diagnostic build of the library: make EXTRA=-DYH_ABLATION OUT=exp_lib/libyolo_hip.so
+OBJDIR=build/abl, then run with YH_LIB=exp_lib/libyolo_hip.so."""
 import ctypes
 import os
 import sys

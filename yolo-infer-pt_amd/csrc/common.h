@@ -112,7 +112,9 @@ struct NmsArgs {
     unsigned* hist;            // [B][2048] coarse score-bin histogram (zeroed by the launcher)
     int bin_base;              // (fp32 bits >> 16) of the lowest bin
     float* dets; int* ndet;
-    unsigned long long* trace;  // optional [B][16] phase timestamps (s_memrealtime), nullptr = off
+#ifdef YH_ABLATION
+    unsigned long long* trace;  // diagnostic builds only: [B][16] phase timestamps (s_memrealtime)
+#endif
 };
 
 // Dense-conv kernel of the fp32 handle (conv.hip). The 16-bit handles run the
@@ -141,8 +143,6 @@ struct HeadClsLevel {
 struct HeadClsArgs {
     HeadClsLevel lv[3];
     int nlv, B, c3, nc;
-    int dbg;                         // experiments (YH_HCLS_DBG): bit k skips phase k (0 dw1 .. 4 pw3)
-    unsigned long long* trace;       // experiments (YH_HCLS_TRACE): [grid][8] s_memrealtime stamps
     const void* zero;                // >= 16 zero bytes (source of out-of-image / padding chunks)
     // direct mode (io != nullptr): pw3's logits leave as sigmoid scores in rows 4.. of the
     // caller's y = io[1] (B, 4+nc, A) instead of the head tensor (the decode's class part)

@@ -61,10 +61,12 @@ struct MxArgs {
     FastDiv d_wo, d_howo;               // KS == 1: flat pixel -> (n, ho, wo)
     FastDiv d_ntw, d_nth, d_nsl;        // task id decomposition
     int M;                              // B * Ho * Wo
-    int dbg;                            // ablation (micro benchmark only): 1 no weight DMA, 2 no patch DMA,
-                                        // 4 no MFMA, 8 no epilogue stores; conv_mxr also 16 no SiLU,
-                                        // 1024 no resident-weight load
-    unsigned long long* trace;          // micro benchmark only: [grid][4] s_memrealtime stamps (nullptr = off)
+#ifdef YH_ABLATION
+    // tools/micro builds only (-DYH_ABLATION; the shipped library has neither field):
+    int dbg;                            // 1 no weight DMA, 2 no patch DMA, 4 no MFMA, 8 no epilogue
+                                        // stores; conv_mxr also 16 no SiLU, 1024 no resident-weight load
+    unsigned long long* trace;          // [grid][4] s_memrealtime stamps (nullptr = off)
+#endif
 };
 
 // One kernel configuration (template parameters of conv_mx).

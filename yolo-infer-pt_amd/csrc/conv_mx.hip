@@ -30,6 +30,16 @@ namespace yh {
 
 typedef __attribute__((ext_vector_type(16))) float f32x16;
 
+// ablation switches of the micro benchmark (tools/micro, -DYH_ABLATION); constant 0 / off
+// in the shipped library
+#ifdef YH_ABLATION
+#define MX_DBG(bit) (p.dbg & (bit))
+#define MX_TRACE (p.trace)
+#else
+#define MX_DBG(bit) 0
+#define MX_TRACE ((unsigned long long*)nullptr)
+#endif
+
 namespace {
 
 // 16-byte LDS-DMA hidden from hipcc's waitcnt pass (ordering: the kernel's own
@@ -183,7 +193,7 @@ __global__ __launch_bounds__(64 * WN * WM, 2) void conv_mx(const MxArgs p) {
     typedef __attribute__((address_space(3))) uint4* lds_p;
     const unsigned lds0 = (unsigned)(size_t)(lds_p)sm4;
 
-    const unsigned long long t_entry = p.trace ? __builtin_amdgcn_s_memrealtime() : 0ull;
+    const unsigned long long t_entry = MX_TRACE ? __builtin_amdgcn_s_memrealtime() : 0ull;
     const int nbi = p.nbi;
     const int stage_ch = ACH + nbi * NT;      // chunks per stage buffer
     const int lane = threadIdx.x & 63;
@@ -322,7 +332,7 @@ __global__ __launch_bounds__(64 * WN * WM, 2) void conv_mx(const MxArgs p) {
         }
         const unsigned sbase = lds0 + (unsigned)(buf * stage_ch * 16);
         // weights: contiguous stage image
-        if (!(p.dbg & 1)) {
+        if (!MX_DBG(1)) {
             const char* wsrc = p.w + ((long long)f_sl * p.nst + st) * p.wstage + (long long)(wv * 64 + lane) * 16;
 #pragma unroll
             for (int i = 0; i < AINS; ++i)
@@ -335,7 +345,7 @@ __global__ __launch_bounds__(64 * WN * WM, 2) void conv_mx(const MxArgs p) {
         const int coff = (seg ? ch0 - p.c0 : ch0) * 2;
         const int clim = (p.cin - ch0) >> 3;   // chunks of this stage inside Cin
         const unsigned bb = sbase + ACH * 16;
-        if (!(p.dbg & 2)) {
+        if (!MX_DBG(2)) {
 #pragma unroll
             for (int i = 0; i < MX_MAXB; ++i) {
                 if (i < nbi) {
@@ -348,7 +358,7 @@ __global__ __launch_bounds__(64 * WN * WM, 2) void conv_mx(const MxArgs p) {
     };
 
     f32x16 acc[NA][MB];
-    const int per_stage = ((p.dbg & 1) ? 0 : AINS) + ((p.dbg & 2) ? 0 : nbi);
+    const int per_stage = (MX_DBG(1) ? 0 : AINS) + (MX_DBG(2) ? 0 : nbi);
     const int co_lane = wn * NA * 32 + 16 * NA * h;   // lane's first cout within the slice
 
     // one stage: NSTEP k-steps, fragments of step s+1 read while step s multiplies
@@ -437,14 +447,14 @@ __global__ __launch_bounds__(64 * WN * WM, 2) void conv_mx(const MxArgs p) {
         }
     };
 
-    unsigned long long t_setup = p.trace ? __builtin_amdgcn_s_memrealtime() : 0ull, t_first = 0;
+    unsigned long long t_setup = MX_TRACE ? __builtin_amdgcn_s_memrealtime() : 0ull, t_first = 0;
     issue(0, 0);
     for (int g = 0; g < nstages; ++g) {
         const bool more = g + 1 < nstages;
         if (more) issue(g + 1, (g + 1) & 1);
         mx_vmwait(more ? per_stage : 0);
         mx_barrier();
-        if (p.trace && g == 0) t_first = __builtin_amdgcn_s_memrealtime();
+        if (MX_TRACE && g == 0) t_first = __builtin_amdgcn_s_memrealtime();
         const int st = g - (g / p.nst) * p.nst;
         if (st == 0) {
 #pragma unroll
@@ -454,12 +464,12 @@ __global__ __launch_bounds__(64 * WN * WM, 2) void conv_mx(const MxArgs p) {
 #pragma unroll
                     for (int e = 0; e < 16; ++e) acc[a][j][e] = 0.f;
         }
-        if (!(p.dbg & 4)) compute((g & 1) * stage_ch);
-        if (st == p.nst - 1 && !(p.dbg & 8)) epilogue(t_lo + g / p.nst);
+        if (!(MX_DBG(4))) compute((g & 1) * stage_ch);
+        if (st == p.nst - 1 && !(MX_DBG(8))) epilogue(t_lo + g / p.nst);
         mx_barrier();
     }
-    if (p.trace && threadIdx.x == 0) {
-        unsigned long long* tr = p.trace + blockIdx.x * 4;
+    if (MX_TRACE && threadIdx.x == 0) {
+        unsigned long long* tr = MX_TRACE + blockIdx.x * 4;
         tr[0] = t_entry; tr[1] = t_setup; tr[2] = t_first; tr[3] = __builtin_amdgcn_s_memrealtime();
     }
 }
@@ -509,7 +519,7 @@ __global__ __launch_bounds__(64 * NW, 2) void conv_mxr(const MxArgs p) {
     // ---- resident weights + bias
     {
         const char* wsrc = p.w + (long long)sl * p.wstage;
-        if (!(p.dbg & 1024))
+        if (!(MX_DBG(1024)))
             for (int q = wv * 64; q < wch; q += 64 * NW)   // wch: a multiple of 64 chunks
                 mx_glds(wsrc + (long long)(q + lane) * 16, lds0 + (unsigned)q * 16);
         if (threadIdx.x < BN / 4)
@@ -643,7 +653,7 @@ __global__ __launch_bounds__(64 * NW, 2) void conv_mxr(const MxArgs p) {
 #pragma unroll
         for (int i = 0; i < NBI; ++i) {
             const int c = (slot_geo[i] >> 22) & 15;
-            const bool ok = sptr[i] != nullptr && c < clim && !(p.dbg & 2);
+            const bool ok = sptr[i] != nullptr && c < clim && !MX_DBG(2);
             mx_glds(ok ? (const void*)(sptr[i] + coff) : (const void*)p.zero, bb + (unsigned)(i * 1024));
         }
     };
@@ -712,7 +722,7 @@ __global__ __launch_bounds__(64 * NW, 2) void conv_mxr(const MxArgs p) {
             for (int a = 0; a < NA; ++a) aj[a] = acc[a][j];
             T* op = out + m * p.ldo + cc;
             const T* rp = res + m * p.ldr + cc;
-            if (p.act == ACT_SILU && !(p.dbg & 16)) {
+            if (p.act == ACT_SILU && !(MX_DBG(16))) {
                 if (res) mx_epi<T, NA, true, true>(aj, bv, op, rp, nc8);
                 else mx_epi<T, NA, true, false>(aj, bv, op, rp, nc8);
             } else {
@@ -741,10 +751,10 @@ __global__ __launch_bounds__(64 * NW, 2) void conv_mxr(const MxArgs p) {
 #pragma unroll
                     for (int e = 0; e < 16; ++e) acc[a][j][e] = 0.f;
         }
-        if (!(p.dbg & 4)) compute(g);
+        if (!(MX_DBG(4))) compute(g);
         // single buffer: the next stage's DMA may only start once this stage's reads are done
         if (NBUF == 1 && more) issue(g + 1);
-        if (st == p.nst - 1 && !(p.dbg & 8)) epilogue(t_lo + g / p.nst);
+        if (st == p.nst - 1 && !(MX_DBG(8))) epilogue(t_lo + g / p.nst);
     }
 }
 

@@ -5,9 +5,6 @@
 // kernels (optionally as one captured HIP graph) and exports the C ABI
 // declared in include/yolo_hip.h.
 #include <hip/hip_runtime.h>
-#include <execinfo.h>
-#include <signal.h>
-#include <unistd.h>
 
 #include <algorithm>
 #include <cmath>
@@ -22,17 +19,6 @@
 #include "common.h"
 #include "conv_mx.h"
 #include "yolo_hip.h"
-
-// YH_SEGV_BT=1 (debugging): print a native backtrace on SIGSEGV before the
-// default handler runs, so a host-side crash inside a call names its frame
-static void segv_bt(int sig) {
-    void* fr[64];
-    const int n = backtrace(fr, 64);
-    (void)!write(2, "[yh] native backtrace:\n", 23);
-    backtrace_symbols_fd(fr, n, 2);
-    signal(sig, SIG_DFL);
-    raise(sig);
-}
 
 
 namespace yh {
@@ -90,6 +76,21 @@ static uint16_t f2h(float f) {
 // ---------------------------------------------------------------- graph model
 enum ConvKind { CK_DENSE = 0, CK_FIRST = 1, CK_DW = 2, CK_PE = 3 };
 enum OpKind { OP_FIRST, OP_CONV, OP_DW, OP_SPPF, OP_ATTN, OP_DECODE, OP_HEADCLS, OP_BOXDFL, OP_CSP, OP_STEM2 };
+static const char* op_kind_name(OpKind k) {
+    switch (k) {
+        case OP_FIRST: return "stem";
+        case OP_CONV: return "conv";
+        case OP_DW: return "dwconv";
+        case OP_SPPF: return "sppf";
+        case OP_ATTN: return "attention";
+        case OP_DECODE: return "decode";
+        case OP_HEADCLS: return "head_cls";
+        case OP_BOXDFL: return "box_dfl";
+        case OP_CSP: return "c3k2";
+        case OP_STEM2: return "stem_fused";
+    }
+    return "unknown";
+}
 enum OpClass { CL_CONV3 = 0, CL_CONV1 = 1, CL_FIRST = 2, CL_DW = 3, CL_SPPF = 4, CL_ATTN = 5, CL_DECODE = 6,
                CL_HEADCLS = 7, CL_BOXDFL = 8, CL_CSP = 9, CL_N = 10 };
 
@@ -154,8 +155,27 @@ struct GraphKey {
     }
 };
 
+// The library's few environment switches, read once per handle at yh_create
+// (INTEGRATION.md lists them): YH_FUSE=0 turns every cross-layer fusion off (the
+// bit-identity tests compare both), YH_CSP_TAIL=1 forces the C3k2 tail mode where
+// the whole block would fit one launch (tested the same way), YH_CONV=<k> forces
+// candidate plan k of every 16-bit dense conv, YH_TUNE_LOG=1 prints the tuner's timings.
+struct Options {
+    bool fuse = true, csp_tail = false, tune_log = false;
+    int conv_force = -1;
+    static Options from_env() {
+        Options o;
+        if (const char* e = getenv("YH_FUSE")) o.fuse = atoi(e) != 0;
+        if (const char* e = getenv("YH_CSP_TAIL")) o.csp_tail = atoi(e) != 0;
+        if (const char* e = getenv("YH_CONV")) o.conv_force = atoi(e);
+        o.tune_log = getenv("YH_TUNE_LOG") != nullptr;
+        return o;
+    }
+};
+
 struct Net {
     yh_variant var;
+    Options opt;
     int device, dtype, es;
     std::vector<Tensor> tensors;
     std::vector<ConvDesc> convs;
@@ -503,10 +523,7 @@ struct Net {
     // the stem and net.p2.0 run fused (conv.hip stem_fused) on 16-bit handles for the
     // instantiated widths (v11_n 16 -> 32, v11_s 32 -> 64)
     bool fuse_stem(int c0, int c1, int c2) const {
-        const char* e = getenv("YH_FUSE");
-        if (dtype == F32 || (e && atoi(e) == 0)) return false;
-        const char* e2 = getenv("YH_FUSE_STEM");
-        if (e2 && atoi(e2) == 0) return false;
+        if (dtype == F32 || !opt.fuse) return false;
         return c0 == 3 && stem2_ok(c1, c2);
     }
     // packed p2.0 parameters of the fused stem: fragments (tile a, step k = cb*9 + tap,
@@ -541,42 +558,22 @@ struct Net {
     // a C3k2 block with one Residual runs fused (c3k2.hip) on 16-bit handles when its input
     // is one plain view of 16-channel blocks and (Cin, c, cout) has an instantiated kernel
     bool fuse_csp(const std::vector<Seg>& in, const std::vector<int>& logical, int c, int out_ch, View out) const {
-        const char* e = getenv("YH_FUSE");
-        if (dtype == F32 || (e && atoi(e) == 0)) return false;
-        const char* e2 = getenv("YH_FUSE_CSP");
-        if (e2 && atoi(e2) == 0) return false;
+        if (dtype == F32 || !opt.fuse) return false;
         if (in.size() != 1 || in[0].up || in[0].v.C != logical[0] || logical[0] % 16 || c % 16 || out_ch % 32) return false;
         if (out.coff % 8 || in[0].v.coff % 8) return false;
         int TH, TW;
         return csp_tile(logical[0] / 16, c / 16, out_ch / 32, 1 << 30, 1 << 30, TH, TW);
     }
     bool fuse_csp_tail(int c, int out_ch, View out) const {
-        const char* e = getenv("YH_FUSE");
-        if (dtype == F32 || (e && atoi(e) == 0)) return false;
-        const char* e2 = getenv("YH_FUSE_CSP");
-        if (e2 && atoi(e2) == 0) return false;
+        if (dtype == F32 || !opt.fuse) return false;
         if (c % 16 || out_ch % 32 || out.coff % 8) return false;
         int TH, TW;
         return csp_tile(0, c / 16, out_ch / 32, 1 << 30, 1 << 30, TH, TW);
     }
-    // YH_CSP_TAIL=1 (experiments): tail mode even where the whole block fits one launch
-    static bool tail_first() {
-        const char* e = getenv("YH_CSP_TAIL");
-        return e && atoi(e) != 0;
-    }
+    // tail mode even where the whole block fits one launch (Options::csp_tail, tests)
+    bool tail_first() const { return opt.csp_tail; }
     static bool csp_tile(int ni, int nc, int no, int H, int W, int& TH, int& TW) {
         static const int cand[][2] = {{8, 16}, {8, 8}, {4, 16}, {4, 8}, {2, 8}, {2, 4}};
-        // YH_CSP_TILE=<TH>x<TW> (experiments): preferred tile when it fits
-        static const std::pair<int, int> pref = [] {
-            int a = 0, b = 0;
-            if (const char* e = getenv("YH_CSP_TILE")) sscanf(e, "%dx%d", &a, &b);
-            return std::make_pair(a, b);
-        }();
-        if (pref.first > 0 && pref.first <= H && pref.second <= W && csp_lds(pref.first, pref.second, ni, nc, no) > 0) {
-            TH = pref.first;
-            TW = pref.second;
-            return true;
-        }
         // the largest tile of >= 64 pixels that leaves room for a second workgroup per CU,
         // else the largest that fits (measured: net.p3.1 at 2x4 tiles, two per CU, 263 us
         // against 68 us at 8x16, one per CU)
@@ -651,8 +648,7 @@ struct Net {
     // the decode folds into box_dfl + head_cls / a class-rows decode (16-bit handles; the
     // box branch's last conv has 4 or 6 16-channel K blocks)
     bool fuse_decode(int boxc, int nc) const {
-        const char* e = getenv("YH_FUSE");
-        if (dtype == F32 || (e && atoi(e) == 0)) return false;
+        if (dtype == F32 || !opt.fuse) return false;
         return (boxc == 64 || boxc == 96) && nc % 4 == 0;
     }
     // first anchor of detect level l (0..2) for an H x W input (make_anchors order)
@@ -664,8 +660,7 @@ struct Net {
     // a level's cls branch is fused when it has 16-channel blocks, 4-channel class groups
     // and an LDS tile next to its resident weights
     bool fuse_head_cls(int C0, int c3, int nc) const {
-        const char* e = getenv("YH_FUSE");
-        if (dtype == F32 || (e && atoi(e) == 0)) return false;
+        if (dtype == F32 || !opt.fuse) return false;
         if (c3 % 16 || nc % 4 || C0 % 16) return false;
         int TH, TW;
         return head_cls_tile(C0, c3, nc, 1 << 30, 1 << 30, TH, TW);
@@ -907,20 +902,7 @@ struct Net {
         a.gm = (a.M + BM - 1) / BM;
         a.gn = (a.Cout + BN - 1) / BN;
         a.zero = zero_dev;
-        a.ks = split_rule(a, BM, BN);
-    }
-    // K split over a workgroup's waves (conv_gemm2k) for 16-bit layers whose BM-64 tiles
-    // number fewer than two per CU and whose K walk is long: a fixed shape rule (the
-    // split rounds differently from the single-chain kernels, so it is never a timing
-    // choice); YH_KSPLIT=0 turns it off.
-    int split_rule(const ConvArgs& a, int BM, int BN) const {
-        static const bool on = [] { const char* e = getenv("YH_KSPLIT"); return !e || atoi(e) != 0; }();
-        if (!on || dtype == F32 || BM != 64 || BN > 128) return 1;
-        const int tiles = a.gm * a.gn, nkt = a.Kp / 64;
-        // measured (r01): 4 slices pay off only for the long walks (head.box.2.0, K = 2304:
-        // 46 -> 33 us); 2 slices on K <= 1152 layers were 10-40 % slower, so they stay off
-        if (tiles >= 512 || nkt < 16 || BN > 64) return 1;
-        return 4;
+        a.ks = 1;
     }
 
     DwArgs dw_args(const Op& op, int B, int H, int W) const {
@@ -1024,9 +1006,8 @@ struct Net {
         auto it = conv_kern.find(key);
         if (it != conv_kern.end()) { cur_kern = &it->second; return; }
         if (!num_cus) HIPCHECK(hipDeviceGetAttribute(&num_cus, hipDeviceAttributeMultiprocessorCount, device));
-        static const int env_forced = [] { const char* e = getenv("YH_CONV"); return e ? atoi(e) : -1; }();
-        const int forced = force_kern >= 0 ? force_kern : env_forced;
-        static const bool tune_log = getenv("YH_TUNE_LOG") != nullptr;
+        const int forced = force_kern >= 0 ? force_kern : opt.conv_force;
+        const bool tune_log = opt.tune_log;
         std::vector<MxChoice> ch(ops.size());
         std::vector<std::vector<MxPlan>> cands(ops.size());
         for (size_t i = 0; i < ops.size(); ++i) {
@@ -1036,18 +1017,6 @@ struct Net {
             conv_args(ops[i], B, H, W, a, BM, BN);
             cands[i] = mx_candidates(mx_shape(a, B), num_cus);
             require(!cands[i].empty(), "no conv_mx plan for " + ops[i].label);
-            // YH_MX_LDS_MAX=<bytes> (experiments): only plans within an LDS budget, leaving
-            // CU room for other streams' kernels (forward lanes); the smallest plan if none fits
-            static const int lds_max = [] { const char* e = getenv("YH_MX_LDS_MAX"); return e ? atoi(e) : 0; }();
-            if (lds_max > 0) {
-                std::vector<MxPlan> keep;
-                for (auto& pl : cands[i])
-                    if (pl.lds <= lds_max) keep.push_back(pl);
-                if (keep.empty())
-                    keep.push_back(*std::min_element(cands[i].begin(), cands[i].end(),
-                                                     [](const MxPlan& x, const MxPlan& y) { return x.lds < y.lds; }));
-                cands[i] = keep;
-            }
             const int pick = forced >= 0 ? std::min(forced, (int)cands[i].size() - 1) : 0;
             ch[i].plan = cands[i][pick];
             ch[i].name = mx_name(ch[i].plan);
@@ -1057,18 +1026,17 @@ struct Net {
         cur_kern = &slot;
         if (forced >= 0) return;
         run_ops(B, H, W, s);
-        // YH_TUNE_INSITU=0 (experiments): time candidates back to back instead
-        static const bool insitu = [] { const char* e = getenv("YH_TUNE_INSITU"); return !e || atoi(e) != 0; }();
         hipEvent_t e0, e1;
         HIPCHECK(hipEventCreate(&e0));
         HIPCHECK(hipEventCreate(&e1));
         for (size_t i = 0; i < ops.size(); ++i) {
             if (ops[i].kind != OP_CONV || cands[i].size() < 2) continue;
-            float best = 1e30f;
-            for (const MxPlan& pl : cands[i]) {
+            std::vector<float> t_ms(cands[i].size(), 0.f);
+            for (size_t c = 0; c < cands[i].size(); ++c) {
+                const MxPlan& pl = cands[i][c];
                 int rc = launch_mx_op(ops[i], pl, B, H, W, s);
                 float ms = 0.f;
-                if (insitu && i > 0) {
+                if (i > 0) {
                     // in situ: each timed launch right after the op that precedes it in the
                     // forward, so the input's cache state (just written, L2 / MALL warm, the
                     // layer's other operands cold) is the forward's, not a back-to-back loop's
@@ -1093,16 +1061,28 @@ struct Net {
                 if (tune_log)
                     fprintf(stderr, "[yh tune] %-36s %-40s %8.2f us\n", ops[i].label.c_str(), mx_name(pl).c_str(),
                             ms * 1e3f / 3);
-                // 3x3: within 3 % of the best time the plan that re-reads fewer input bytes wins
-                // (halo and cout-slice re-reads; stable choices, less HBM pressure beside other lanes)
-                const bool faster = ms < best * 0.97f;
-                const bool tie = pl.cfg.ks == 3 && ms < best * 1.03f && patch_reads(pl) < patch_reads(slot[i].plan);
-                if (best >= 1e29f || faster || tie) {
-                    best = std::min(best, ms);
-                    slot[i].plan = pl;
-                    slot[i].name = mx_name(pl);
-                }
+                t_ms[c] = ms;
             }
+            // pick after every candidate is timed: the fastest, except that for 3x3 layers a plan
+            // within 3 % of the fastest that re-reads fewer input bytes (halo and cout-slice
+            // re-reads) wins - stable choices, less HBM pressure beside the other lanes
+            const float best = *std::min_element(t_ms.begin(), t_ms.end());
+            size_t pick = 0;
+            for (size_t c = 0; c < cands[i].size(); ++c) {
+                const MxPlan &pc = cands[i][c], &pp = cands[i][pick];
+                const bool near = pc.cfg.ks == 3 && t_ms[c] <= best * 1.03f;
+                const bool near_p = pp.cfg.ks == 3 && t_ms[pick] <= best * 1.03f;
+                bool better;
+                if (near && near_p) {
+                    const double rc_ = patch_reads(pc), rp = patch_reads(pp);
+                    better = rc_ < rp || (rc_ == rp && t_ms[c] < t_ms[pick]);
+                } else {
+                    better = (near && !near_p) || (!near_p && t_ms[c] < t_ms[pick]);
+                }
+                if (better) pick = c;
+            }
+            slot[i].plan = cands[i][pick];
+            slot[i].name = mx_name(cands[i][pick]);
         }
         (void)hipEventDestroy(e0);
         (void)hipEventDestroy(e1);
@@ -1142,7 +1122,6 @@ struct Net {
             v.ntw = (v.W + v.TW - 1) / v.TW;
             v.tiles = v.ntw * ((v.H + v.TH - 1) / v.TH);
         }
-        if (const char* e = getenv("YH_HCLS_DBG")) a.dbg = atoi(e);
         a.zero = zero_dev;
         if (op.direct) {
             a.io = (const void* const*)io_dev;
@@ -1223,44 +1202,7 @@ struct Net {
             case OP_SPPF: rc = launch_sppf(dtype, pool_args(op, B, H, W), s); break;
             case OP_ATTN: rc = launch_attention(dtype, attn_args(op, H, W), B, s); break;
             case OP_HEADCLS: {
-                HeadClsArgs a = head_cls_args(op, B, H, W);
-                // YH_HCLS_TRACE=1 (experiments, eager launches only): per-workgroup phase stamps
-                static const bool trace = getenv("YH_HCLS_TRACE") != nullptr;
-                hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
-                (void)hipStreamIsCapturing(s, &cs);
-                static unsigned long long* tbuf = nullptr;
-                int grid = 0;
-                for (int l = 0; l < a.nlv; ++l) grid += B * a.lv[l].tiles;
-                if (trace && cs == hipStreamCaptureStatusNone) {
-                    static int cap = 0;
-                    if (grid > cap) {
-                        if (tbuf) (void)hipFree(tbuf);
-                        HIPCHECK(hipMalloc(&tbuf, (size_t)grid * 64));
-                        cap = grid;
-                    }
-                    a.trace = tbuf;
-                }
-                rc = launch_head_cls(dtype, a, s);
-                if (rc == 0 && a.trace) {
-                    HIPCHECK(hipStreamSynchronize(s));
-                    std::vector<unsigned long long> h((size_t)grid * 8);
-                    HIPCHECK(hipMemcpy(h.data(), tbuf, h.size() * 8, hipMemcpyDeviceToHost));
-                    unsigned long long t0 = ~0ull, t1 = 0;
-                    std::vector<double> ph[6];
-                    for (int g = 0; g < grid; ++g) {
-                        const unsigned long long* r = &h[(size_t)g * 8];
-                        t0 = std::min(t0, r[0]);
-                        t1 = std::max(t1, r[6]);
-                        for (int k = 0; k < 6; ++k) ph[k].push_back((r[k + 1] - r[k]) * 0.01);
-                    }
-                    fprintf(stderr, "[head_cls] span %.1f us, per-WG phase medians (us):", (t1 - t0) * 0.01);
-                    static const char* nm[6] = {"load", "dw1", "pw1", "dw2", "pw2", "pw3"};
-                    for (int k = 0; k < 6; ++k) {
-                        std::sort(ph[k].begin(), ph[k].end());
-                        fprintf(stderr, " %s %.2f", nm[k], ph[k][ph[k].size() / 2]);
-                    }
-                    fprintf(stderr, "\n");
-                }
+                rc = launch_head_cls(dtype, head_cls_args(op, B, H, W), s);
                 break;
             }
             case OP_DECODE: {
@@ -1320,8 +1262,7 @@ struct Net {
                 a.zero = zero_dev;
                 if (!num_cus) HIPCHECK(hipDeviceGetAttribute(&num_cus, hipDeviceAttributeMultiprocessorCount, device));
                 // two workgroups per CU when the LDS allows (measured: net.p2.1 138 -> 103 us at b32)
-                static const int per_cu = [] { const char* e = getenv("YH_CSP_WG_PER_CU"); return e ? atoi(e) : 2; }();
-                rc = launch_csp(dtype, a, std::min(a.ntiles, per_cu * num_cus), s);
+                rc = launch_csp(dtype, a, std::min(a.ntiles, 2 * num_cus), s);
                 break;
             }
         }
@@ -1344,17 +1285,6 @@ struct Net {
     }
     void launch_unit(const Unit& u, int B, int H, int W, hipStream_t s) {
         for (int k = u.first; k < u.last; ++k) launch_op(k, B, H, W, s);
-        // YH_SYNC_UNITS=1 (debugging): synchronize after every launch unit outside graph
-        // capture, so a device fault is reported with the unit that caused it
-        static const bool sync_units = getenv("YH_SYNC_UNITS") != nullptr;
-        if (sync_units) {
-            hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
-            (void)hipStreamIsCapturing(s, &st);
-            if (st == hipStreamCaptureStatusNone) {
-                const hipError_t e = hipStreamSynchronize(s);
-                if (e != hipSuccess) throw Fail(YH_EHIP, "unit " + ops[u.first].label + ": " + hipGetErrorString(e));
-            }
-        }
     }
 
     void run_ops(int B, int H, int W, hipStream_t s) {
@@ -1368,13 +1298,6 @@ struct Net {
     int in_u8 = 0;   // the current forward's input kind (see GraphKey::X)
     void forward(const void* x, int B, int H, int W, void* y, hipStream_t s, int x_u8 = 0) {
         in_u8 = x_u8;
-        static const bool bt = getenv("YH_SEGV_BT") != nullptr;
-        if (bt) {
-            struct sigaction sa {};
-            sa.sa_handler = segv_bt;
-            sa.sa_flags = SA_RESETHAND;
-            sigaction(SIGSEGV, &sa, nullptr);
-        }
         for (auto& d : convs) require(d.loaded, "weights of " + d.name + " not loaded", YH_ESTATE);
         reserve(B, H, W);
         HIPCHECK(hipSetDevice(device));
@@ -1428,12 +1351,9 @@ struct Net {
                 if (g) (void)hipGraphDestroy(g);
                 throw;
             }
-            if (bt) fprintf(stderr, "[yh] captured B=%d H=%d W=%d\n", B, H, W);
             HIPCHECK(hipStreamEndCapture(cap_stream, &g));
-            if (bt) fprintf(stderr, "[yh] capture ended\n");
             hipGraphExec_t ex = nullptr;
             HIPCHECK(hipGraphInstantiate(&ex, g, nullptr, nullptr, 0));
-            if (bt) fprintf(stderr, "[yh] instantiated\n");
             (void)hipGraphDestroy(g);
             it = graphs.emplace(key, ex).first;
         }
@@ -1631,6 +1551,7 @@ int yh_create(const yh_variant* v, int device, int dtype, yh_handle** out) {
         std::unique_ptr<yh_handle> h(new yh_handle());
         yh::Net& n = h->net;
         n.var = *v;
+        n.opt = yh::Options::from_env();
         n.device = device;
         n.dtype = dtype;
         n.es = yh::dtype_size(dtype);
@@ -1724,14 +1645,16 @@ size_t yh_nms_workspace_bytes(int batch, int num_classes, int anchors) {
     return (size_t)batch * anchors * num_classes * 8 + (size_t)batch * 4 + (size_t)batch * 2048 * 4 + 512;
 }
 
-// Debug hook (not part of the ABI header): yh_debug_nms_trace(buf) makes later
-// yh_nms calls record per-image phase timestamps into the device buffer buf
-// ([batch][16] u64, s_memrealtime ticks at 100 MHz); nullptr turns it off.
+#ifdef YH_ABLATION
+// Diagnostic builds only (make EXTRA=-DYH_ABLATION; not in the ABI header):
+// yh_debug_nms_trace(buf) makes later yh_nms calls record per-image phase timestamps
+// into the device buffer buf ([batch][16] u64, s_memrealtime ticks at 100 MHz).
 static unsigned long long* nms_trace = nullptr;
 extern "C" int yh_debug_nms_trace(void* device_buf) {
     nms_trace = (unsigned long long*)device_buf;
     return 0;
 }
+#endif
 
 int yh_nms(int dtype, const void* y, int batch, int num_classes, int anchors, float conf_threshold,
            double iou_threshold, int max_det, int max_nms, float max_wh, void* workspace, size_t workspace_bytes,
@@ -1767,7 +1690,9 @@ int yh_nms(int dtype, const void* y, int batch, int num_classes, int anchors, fl
         a.max_wh = max_wh;
         a.max_det = max_det;
         a.max_nms = max_nms;
+#ifdef YH_ABLATION
         a.trace = nms_trace;
+#endif
         a.keys = (unsigned long long*)workspace;
         a.counts = (int*)((char*)workspace + (size_t)batch * anchors * num_classes * 8);
         a.hist = (unsigned*)((char*)workspace + (((size_t)batch * anchors * num_classes * 8 + (size_t)batch * 4 + 255) & ~(size_t)255));
@@ -1848,10 +1773,9 @@ int yh_op_kernel(const yh_handle* h, int index, int batch, int height, int width
     return guarded([&] {
         yh::require(h && index >= 0 && index < (int)h->net.ops.size(), "op index out of range");
         const yh::Net& n = h->net;
-        static const char* op_names[] = {"stem", "conv", "dwconv", "sppf", "attention", "decode", "head_cls", "box_dfl", "c3k2"};
         const yh::Op& op = n.ops[index];
         if (op.kind != yh::OP_CONV) {
-            if (name) *name = op_names[(int)op.kind];
+            if (name) *name = yh::op_kind_name(op.kind);
             return;
         }
         if (n.dtype == yh::F32) {

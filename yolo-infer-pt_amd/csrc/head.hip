@@ -15,8 +15,6 @@
 // conv_mx's K order (16-channel blocks ascending, one v_mfma_f32_32x32x16 step each, fp32
 // accumulator, + bias, activation, one rounding). The first pointwise output is zeroed
 // outside the image: it is the second depthwise conv's zero padding.
-#include <cstdlib>
-
 #include "common.h"
 #include "dtypes.h"
 
@@ -224,10 +222,6 @@ __device__ __forceinline__ void hc_pw_run(const T* src, int ss, int NPX, const T
 // the registers allow).
 template <typename T, int NK1, int NAP1, int NK2>
 __device__ __forceinline__ void hc_body(const HeadClsArgs& A, int li, char* hsm) {
-    unsigned long long st[8];
-    const bool tr = A.trace != nullptr;
-    auto stamp = [&](int i) { if (tr) st[i] = __builtin_amdgcn_s_memrealtime(); };
-    stamp(0);
     const HeadClsLevel& V = A.lv[li];
     const int wl = blockIdx.x - V.wg0;
     const int n = wl / V.tiles, tix = wl - n * V.tiles;
@@ -292,16 +286,11 @@ __device__ __forceinline__ void hc_body(const HeadClsArgs& A, int li, char* hsm)
             }
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's DMAs (and earlier loads) landed
-        stamp(1);
-        if (!(A.dbg & 1)) hc_dw<T>(R1, XW, L.SX, R2, MH, MW, L.SD, cl, ck, PW1, C0, PB1);
-        else hc_barrier();
-        stamp(2);
+        hc_dw<T>(R1, XW, L.SX, R2, MH, MW, L.SD, cl, ck, PW1, C0, PB1);
         if (cl + ck < C0) hc_barrier();   // the next chunk overwrites R1
     }
     // 3. pw1: D1 (R2) -> P1 (R1), zero outside the image (dw2's zero padding)
-    if (A.dbg & 2) hc_barrier();
-    else
-        hc_pw_run<T, NK1, NAP1>(R2, L.SD, MH * MW, reinterpret_cast<const T*>(V.pw1w), V.pw1ld, QB1, c3, true, A1,
+    hc_pw_run<T, NK1, NAP1>(R2, L.SD, MH * MW, reinterpret_cast<const T*>(V.pw1w), V.pw1ld, QB1, c3, true, A1,
                                 [&](int px, int co, uint2 v) {
                                     const int r = px / MW, cc = px - r * MW;
                                     const int gh = h0 - 1 + r, gw = w0 - 1 + cc;
@@ -311,24 +300,17 @@ __device__ __forceinline__ void hc_body(const HeadClsArgs& A, int li, char* hsm)
                                 });
     HcA<NK2, HC_NA> A2;   // pw2's weights, in flight during dw2
     hc_pw_pre<T, NK2, HC_NA>(reinterpret_cast<const T*>(V.pw2w), V.pw2ld, c3, A2);
-    stamp(3);
     // 4. dw2 (opens with the barrier after pw1): P1 (R1) -> D2 (R2) over the TH x TW tile
-    if (!(A.dbg & 4)) hc_dw<T>(R1, MW, L.SM, R2, TH, TW, L.SM, 0, c3, PW2, c3, PB2);
-    else hc_barrier();
-    stamp(4);
+    hc_dw<T>(R1, MW, L.SM, R2, TH, TW, L.SM, 0, c3, PW2, c3, PB2);
     // 5. pw2: D2 (R2) -> P2 (R1)
-    if (A.dbg & 8) hc_barrier();
-    else
-        hc_pw_run<T, NK2, HC_NA>(R2, L.SM, TH * TW, reinterpret_cast<const T*>(V.pw2w), V.pw2ld, QB2, c3, true, A2,
+    hc_pw_run<T, NK2, HC_NA>(R2, L.SM, TH * TW, reinterpret_cast<const T*>(V.pw2w), V.pw2ld, QB2, c3, true, A2,
                                  [&](int px, int co, uint2 v) { *reinterpret_cast<uint2*>(R1 + px * L.SM + co) = v; });
     HcA<NK2, HC_NA> A3;   // pw3's weights: issued once pw2's are dead
     hc_pw_pre<T, NK2, HC_NA>(reinterpret_cast<const T*>(V.pw3w), V.pw3ld, A.nc, A3);
-    stamp(5);
     // 6. pw3: P2 (R1) -> class logits in the head tensor, or (direct mode) their sigmoid in
     //    the caller's y, one row per class (the decode's class part: logit rounded first)
     T* y = reinterpret_cast<T*>(V.y);
-    if (A.dbg & 16) hc_barrier();
-    else if (A.io)
+    if (A.io)
         hc_pw_run<T, NK2, HC_NA>(R1, L.SM, TH * TW, reinterpret_cast<const T*>(V.pw3w), V.pw3ld, QB3, A.nc, false,
                                  A3, [&](int px, int co, uint2 v) {
                                      const int r = px / TW, cc = px - r * TW;
@@ -350,12 +332,6 @@ __device__ __forceinline__ void hc_body(const HeadClsArgs& A, int li, char* hsm)
                                      if ((unsigned)gh < (unsigned)H && (unsigned)gw < (unsigned)W)
                                          *reinterpret_cast<uint2*>(y + (((long long)n * H + gh) * W + gw) * V.ldy + co) = v;
                                  });
-    stamp(6);
-    if (tr && threadIdx.x == 0) {
-        unsigned long long* o = A.trace + (size_t)blockIdx.x * 8;
-        for (int k = 0; k < 7; ++k) o[k] = st[k];
-        o[7] = (unsigned long long)li;
-    }
 }
 
 template <typename T>
@@ -499,9 +475,7 @@ int head_cls_lds(int TH, int TW, int C0, int c3, int nc) {
     // parameter chunks: 10 (C0 + c3) / 4 + 72 <= 4 per thread
     if ((10 * (C0 + c3)) / 4 + 72 > 4 * HEAD_CLS_THREADS) return 0;
     const HcLayout L = hc_layout(TH, TW, C0, c3);
-    // YH_HCLS_LDS=<bytes> (experiments): tile LDS budget (default HEAD_CLS_LDS)
-    static const int budget = [] { const char* e = getenv("YH_HCLS_LDS"); return e ? atoi(e) : HEAD_CLS_LDS; }();
-    return L.total <= budget && L.total <= 160 * 1024 ? L.total : 0;
+    return L.total <= HEAD_CLS_LDS && L.total <= 160 * 1024 ? L.total : 0;
 }
 
 template <typename T>

@@ -27,6 +27,14 @@
 
 #pragma clang fp contract(off)
 
+// phase stamps of the diagnostic build (make EXTRA=-DYH_ABLATION, tools/nms_trace.py);
+// compiled out of the shipped library
+#ifdef YH_ABLATION
+#define NMS_TRACE (p.trace)
+#else
+#define NMS_TRACE ((unsigned long long*)nullptr)
+#endif
+
 namespace yh {
 
 namespace {
@@ -322,7 +330,7 @@ __device__ void nms_batch(NmsSmem& S, const NmsArgs& p, const T* y, float* dets,
         const int n = blockIdx.x;
         int sbi = 0;
         const IouThr th = make_thr(p.iou);
-#define SB_MARK(k) do { if (p.trace && tid == 0 && sbi == 0) p.trace[n * 16 + (k)] = __builtin_amdgcn_s_memrealtime(); } while (0)
+#define SB_MARK(k) do { if (NMS_TRACE && tid == 0 && sbi == 0) NMS_TRACE[n * 16 + (k)] = __builtin_amdgcn_s_memrealtime(); } while (0)
         for (int s0 = 0; s0 < want && S.kept < p.max_det; s0 += SB) {
             const int ns = min(SB, want - s0);
             if (tid < ns) {
@@ -521,7 +529,7 @@ __device__ unsigned block_scan_incl(NmsSmem& S, unsigned v, int lane, int wave) 
 
 #define NMS_MARK(k)                                                                       \
     do {                                                                                  \
-        if (p.trace && tid == 0) p.trace[n * 16 + (k)] = __builtin_amdgcn_s_memrealtime(); \
+        if (NMS_TRACE && tid == 0) NMS_TRACE[n * 16 + (k)] = __builtin_amdgcn_s_memrealtime(); \
     } while (0)
 
 template <typename T>
@@ -536,7 +544,7 @@ __global__ __launch_bounds__(NMS_T) void nms_image(const NmsArgs p) {
     const int ktot = min(nall, p.max_nms);
     if (tid == 0) S.kept = 0;
     NMS_MARK(0);
-    if (p.trace && tid == 0) p.trace[n * 16 + 7] = __builtin_amdgcn_s_memtime();
+    if (NMS_TRACE && tid == 0) NMS_TRACE[n * 16 + 7] = __builtin_amdgcn_s_memtime();
 
     // C[b] = number of candidates in score bins >= b (suffix sums of the emitted histogram)
     unsigned* C = S.hist;  // C[0..NBINS], C[NBINS] = 0
@@ -605,7 +613,7 @@ __global__ __launch_bounds__(NMS_T) void nms_image(const NmsArgs p) {
         __syncthreads();
     }
     NMS_MARK(5);
-    if (p.trace && tid == 0) { p.trace[n * 16 + 8] = nbatch; p.trace[n * 16 + 9] = processed; p.trace[n * 16 + 11] = nall; }
+    if (NMS_TRACE && tid == 0) { NMS_TRACE[n * 16 + 8] = nbatch; NMS_TRACE[n * 16 + 9] = processed; NMS_TRACE[n * 16 + 11] = nall; }
     if (fallback) {
         // ---- general path: radix-select the next <= CAP keys below ub (exact for any ties)
         while (processed < ktot && S.kept < p.max_det) {
@@ -683,7 +691,7 @@ __global__ __launch_bounds__(NMS_T) void nms_image(const NmsArgs p) {
         }
     }
     NMS_MARK(6);
-    if (p.trace && tid == 0) p.trace[n * 16 + 10] = __builtin_amdgcn_s_memtime();
+    if (NMS_TRACE && tid == 0) NMS_TRACE[n * 16 + 10] = __builtin_amdgcn_s_memtime();
     if (tid == 0) p.ndet[n] = S.kept;
 }
 

@@ -16,8 +16,13 @@
 //   and s >= src - 1 -> (src - 1, f 0) on the x axis (rows are clamped instead);
 //   11-bit coefficients a0 = rint((1 - f) 2048), a1 = rint(f 2048);
 //   horizontal pass in int: H = S[s] a0 + S[s + 1] a1;
-//   vertical pass as OpenCV's vector kernel computes it (x86 builds):
-//   out = sat_u8((mulhi16(H0 >> 4, b0) + mulhi16(H1 >> 4, b1) + 2) >> 2).
+//   vertical pass as OpenCV's vector kernel computes it (VResizeLinearVec_32s8u, x86
+//   builds with 128-bit universal intrinsics):
+//   out = sat_u8((mulhi16(H0 >> 4, b0) + mulhi16(H1 >> 4, b1) + 2) >> 2)
+//   over the row's bytes the vector loops cover (16-byte steps while x <= width - 16,
+//   then one 8-byte step while x < width - 8, width = 3 nw bytes); the remaining tail
+//   bytes take the scalar FixedPtCast: out = sat_u8((H0 b0 + H1 b1 + 2^21) >> 22).
+//   Which vector width the cv2 build used is an assumption (parity unpinned vs cv2).
 //   Exactly 2x downscales on both axes take INTER_AREA's fast path
 //   ((S00 + S01 + S10 + S11 + 2) >> 2), as cv2.resize does.
 #include <cmath>
@@ -60,6 +65,14 @@ __host__ __device__ inline LbAxis lb_axis(int d, int src, double scale, bool cla
 
 __host__ __device__ inline int lb_mulhi(int a, int b) { return (a * b) >> 16; }
 
+// first byte of a resized row (width = 3 nw bytes) that OpenCV's vertical pass computes
+// with its scalar loop instead of VResizeLinearVec_32s8u (see the header comment)
+__host__ __device__ inline int lb_vtail(int width) {
+    int x = width >= 16 ? ((width - 16) / 16 + 1) * 16 : 0;
+    if (x < width - 8) x += 8;
+    return x;
+}
+
 // Pixel (y, x) of the letterboxed canvas, 3 channels in RGB order.
 __host__ __device__ inline void lb_pixel(const LbImage& im, int y, int x, unsigned char rgb[3]) {
     rgb[0] = rgb[1] = rgb[2] = 0;
@@ -83,10 +96,12 @@ __host__ __device__ inline void lb_pixel(const LbImage& im, int y, int x, unsign
     const LbAxis ay = lb_axis(dy, im.h, sy, false);
     const unsigned char* r0 = S + (size_t)ay.s0 * im.stride;
     const unsigned char* r1 = S + (size_t)ay.s1 * im.stride;
+    const int tail = lb_vtail(3 * im.nw);
     for (int c = 0; c < 3; ++c) {
         const int h0 = r0[ax.s0 * 3 + c] * ax.a0 + r0[ax.s1 * 3 + c] * ax.a1;
         const int h1 = r1[ax.s0 * 3 + c] * ax.a0 + r1[ax.s1 * 3 + c] * ax.a1;
-        int v = (lb_mulhi(h0 >> 4, ay.a0) + lb_mulhi(h1 >> 4, ay.a1) + 2) >> 2;
+        int v = dx * 3 + c < tail ? (lb_mulhi(h0 >> 4, ay.a0) + lb_mulhi(h1 >> 4, ay.a1) + 2) >> 2
+                                  : (h0 * ay.a0 + h1 * ay.a1 + (1 << 21)) >> 22;
         v = v < 0 ? 0 : (v > 255 ? 255 : v);
         rgb[2 - c] = (unsigned char)v;
     }

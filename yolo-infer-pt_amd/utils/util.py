@@ -36,32 +36,9 @@ from yolo_hip.metrics import compute_ap, compute_metric, smooth  # noqa: F401
 __all__ = ["setup_seed", "setup_multi_processes", "wh2xy", "make_anchors", "non_max_suppression", "load_weight",
            "load_ultralytics_weight", "compute_metric", "compute_ap", "smooth", "AverageMeter"]
 
-# Training-side names of the reference's utils/util.py (losses, label assigner, EMA,
-# LR schedules, optimizer groups, plots, ONNX export, checkpoint stripping): outside
-# this build's scope. They exist here so the reference's module
-# surface is complete, and fail loudly when used.
-OUT_OF_SCOPE = ("Assigner", "BoxLoss", "ComputeLoss", "CosineLR", "EMA", "FocalLoss", "LinearLR", "QFL", "VFL",
-                "clip_gradients", "compute_iou", "export_onnx", "plot_curve", "plot_lr", "plot_pr_curve",
-                "set_params", "strip_optimizer")
-
-
-def _out_of_scope(name, ref):
-    def stub(*args, **kwargs):
-        raise NotImplementedError(f"utils.util.{name} ({ref} in the reference) is training-side and outside this "
-                                  f"inference build's scope; use the reference's own utils for training")
-    stub.__name__ = stub.__qualname__ = name
-    stub.__doc__ = f"Out of scope: the reference's {ref} (training side). Raises NotImplementedError."
-    return stub
-
-
-for _name, _ref in zip(OUT_OF_SCOPE, ("utils/util.py:643", "utils/util.py:798", "utils/util.py:831",
-                                      "utils/util.py:559", "utils/util.py:599", "utils/util.py:775",
-                                      "utils/util.py:581", "utils/util.py:738", "utils/util.py:749",
-                                      "utils/util.py:340", "utils/util.py:303", "utils/util.py:47",
-                                      "utils/util.py:202", "utils/util.py:537", "utils/util.py:180",
-                                      "utils/util.py:519", "utils/util.py:332")):
-    globals()[_name] = _out_of_scope(_name, _ref)
-del _name, _ref
+# Training-side names of the reference's utils/util.py (losses, label assigner, EMA, LR
+# schedules, optimizer groups, plots, ONNX export) are outside this build's scope
+#  and deliberately absent: training keeps the reference's own utils.
 
 
 class AverageMeter:
