@@ -69,9 +69,14 @@ def roofline(eng, args, batch, prof_steps, x, y):
         c["bytes"] += o["bytes"]
         c["flops"] += o["flops"]
         c["launches"] += 1
-        peak_tf = MFMA_PEAK_TFLOPS[args.dtype] if o["cls"] in ("conv3x3", "conv1x1") else 157.3
+        # every class is scored against the roof of the arithmetic it runs: the 16-bit handles'
+        # kernels (convs and every fused kernel) run bf16/fp16 MFMA, the fp32 handle fp32/fp64
+        peak_tf = MFMA_PEAK_TFLOPS[args.dtype]
         c["attain_ms"] += max(o["bytes"] / (HBM_PEAK_GBS * 1e9), o["flops"] / (peak_tf * 1e12)) * 1e3
     total = sum(c["ms"] for c in by_cls.values())
+    total_bytes = sum(c["bytes"] for c in by_cls.values())
+    total_flops = sum(c["flops"] for c in by_cls.values())
+    total_attain = sum(c["attain_ms"] for c in by_cls.values())
     for k, c in sorted(by_cls.items(), key=lambda kv: -kv[1]["ms"]):
         log(f"  {k:10s} {c['launches']:3d} launches  {c['ms'] * 1e3:8.1f} us/fwd ({100 * c['ms'] / total:4.1f}%)  "
             f"{c['bytes'] / c['ms'] / 1e6:7.0f} GB/s  {c['flops'] / c['ms'] / 1e9:7.1f} TFLOP/s  "
@@ -98,7 +103,19 @@ def roofline(eng, args, batch, prof_steps, x, y):
                 avg_launch_us=round(dom["ms"] * 1e3 / dom["launches"], 2),
                 algorithmic_bytes_per_launch=round(dom["bytes"] / dom["launches"]),
                 attainable_frac=round(dom["attain_ms"] / dom["ms"], 4),
-                forward_kernel_ms=round(total, 4))
+                forward_kernel_ms=round(total, 4),
+                # the whole forward against HBM: algorithmic bytes of every op per forward over the
+                # summed kernel time (HIP events, one forward at a time) and 8 TB/s
+                forward=dict(algorithmic_bytes=round(total_bytes), algorithmic_flops=round(total_flops),
+                             kernel_ms=round(total, 4),
+                             achieved_GBs=round(total_bytes / total / 1e6, 1),
+                             frac_hbm=round(total_bytes / total / 1e6 / HBM_PEAK_GBS, 4),
+                             attainable_frac=round(total_attain / total, 4),
+                             launches=sum(c["launches"] for c in by_cls.values())),
+                per_class={k: dict(launches=c["launches"], us=round(c["ms"] * 1e3, 1),
+                                   algorithmic_MB=round(c["bytes"] / 1e6, 2),
+                                   attainable_frac=round(c["attain_ms"] / c["ms"], 4))
+                           for k, c in by_cls.items()})
 
 
 PMC_SUMMARY = os.path.join(ROOT, "profiles", "pmc_traffic_latest.json")
@@ -135,13 +152,14 @@ def _cpu_model():
 
 
 def cpu_baseline(args, runs=3):
-    """the build's CPU restatement (oracle/, fp32 functional forward with BN
-    folded + numpy NMS) on one batch of the bench's size, torch.inference_mode(), every host
-    core this process may use, one warm-up then the median of `runs` timed runs."""
+    """the build's CPU restatement of the forward (oracle/, fp32 functional
+    forward with BN folded, torch.inference_mode()) plus the library's C++ host NMS (yh_nms_host,
+    the contract torchvision's C++ kernel fills in the reference) on one batch of the bench's size,
+    every host core this process may use, one warm-up then the median of `runs` timed runs. The
+    forward and the NMS are timed separately and reported both apart and together."""
     import statistics
-    import numpy as np
-    from oracle import nms as onms
     from oracle.forward import Oracle
+    from yolo_hip.engine import nms_host
     from yolo_hip.variants import VARIANTS
 
     # cores this process may use: the box's CPU share (OMP_NUM_THREADS is set to it there;
@@ -158,23 +176,27 @@ def cpu_baseline(args, runs=3):
     orc = Oracle(model.state_dict(), v.width, v.depth, v.csp, 80, dtype=torch.float32)
     B = args.batch
     g = torch.Generator().manual_seed(0)
-    x = torch.rand(B, 3, args.size, args.size, generator=g)   # BASELINE.md §3 inputs
+    x = torch.rand(B, 3, args.size, args.size, generator=g)   # BASELINE.md section 3 inputs
 
     def once():
         t0 = time.perf_counter()
         with torch.inference_mode():
             y = orc(x)
-        onms.non_max_suppression(np.ascontiguousarray(y.numpy()))
-        return time.perf_counter() - t0
+        t1 = time.perf_counter()
+        nms_host(y, threads=threads)
+        return t1 - t0, time.perf_counter() - t1
 
     once()   # warm-up
-    times = [once() for _ in range(runs)]
-    med = statistics.median(times)
-    return dict(value=round(B / med, 3), unit="images/s", cores=threads, kind="port",
+    res = [once() for _ in range(runs)]
+    fwd = statistics.median(r[0] for r in res)
+    nms_s = statistics.median(r[1] for r in res)
+    tot = statistics.median(r[0] + r[1] for r in res)
+    return dict(value=round(B / tot, 3), unit="images/s", cores=threads, kind="port",
                 cpu_model=_cpu_model(), host_cpus_visible=os.cpu_count(),
-                runs_s=[round(t, 3) for t in times],
+                forward_images_per_s=round(B / fwd, 3), forward_s=round(fwd, 3),
+                nms_s=round(nms_s, 4), runs_s=[round(r[0] + r[1], 3) for r in res],
                 sample=f"batch {B} (torch.rand seed 0, {args.size}x{args.size}), v11_{args.variant} fp32 oracle "
-                       f"forward (BN folded) + numpy NMS; 1 warm-up + median of {runs} runs, "
+                       f"forward (BN folded) + C++ host NMS (yh_nms_host); 1 warm-up + median of {runs} runs, "
                        f"{threads} threads, torch.inference_mode()")
 
 
@@ -196,6 +218,8 @@ def main():
                          "(measured r01, v11_n b32: 1 -> 20.3k, 2 -> 23.2k, 3 -> 27.2k, 4 -> 25.2k img/s)")
     ap.add_argument("--nms-on-lane", action="store_true",
                     help="run each batch's NMS on its forward lane's stream (no separate NMS stream)")
+    ap.add_argument("--input-ring", type=int, default=4,
+                    help="distinct input batches the timed steps cycle through (> 256 MB of MALL in total)")
     ap.add_argument("--serial", action="store_true",
                     help="run forward and NMS back to back on one stream (no batch-to-batch overlap)")
     args = ap.parse_args()
@@ -224,8 +248,12 @@ def main():
     eng.load_module(model)
     B, S = args.batch, args.size
     eng.reserve(B, S, S)
-    # synthetic scenes, one distinct batch per rank, resident in HBM before timing
-    x = synth.synth_scenes(B, S, S, seed=100 + rank).to(dev, dtype)
+    # synthetic scenes resident in HBM before timing: a ring of distinct batches per rank whose
+    # total (4 x 78.6 MB at v11_n b32 640^2 bf16) exceeds the 256 MB MALL, so a step's input is
+    # not left in the last-level cache by an earlier step
+    ring = max(1, args.input_ring)
+    xs = [synth.synth_scenes(B, S, S, seed=100 + rank + 1000 * k).to(dev, dtype) for k in range(ring)]
+    x = xs[0]
     A = eng.num_anchors(S, S)
     y = torch.empty((B, 84, A), dtype=dtype, device=dev)
     gather = Gather(B, 300, dev, rank, world, slots=2 * args.lanes + 2)   # >= batches in flight
@@ -242,14 +270,18 @@ def main():
         torch.cuda.synchronize()
     pipe = DetectPipeline(engs, B, S, S, post=post, nms_on_lane=args.nms_on_lane)
 
+    it = [0]
+
     def step():
+        xk = xs[it[0] % ring]
+        it[0] += 1
         if args.serial:
-            eng.forward(x, out=y)
+            eng.forward(xk, out=y)
             dets, counts = nms(y)
             extra = post(dets, counts) if dist else None
             return dets, counts, extra
         # forward of this batch overlaps the NMS (+ gather) of the previous one
-        return pipe.submit(x)[:3]
+        return pipe.submit(xk)[:3]
 
     for _ in range(args.warmup):
         step()
@@ -305,7 +337,7 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": args.dtype,
-            "data": "synthetic (seeded scenes; calibrated synthetic weights)",
+            "data": f"synthetic (seeded scenes, a ring of {ring} distinct batches; calibrated synthetic weights)",
             "config": {"workload": f"yolo_v11_{args.variant} eval forward + NMS, {S}x{S}, {B} images per GPU per step",
                        "per_gpu_batch": B, "global_batch": B * world, "image_size": S,
                        "parallelism": f"dp{world}", "nms": "on-device, conf 0.001, iou 0.65, max_det 300"},

@@ -7,8 +7,20 @@ Tolerances (written here, justified in DESIGN.md §Parity):
            by the stride), widened to 2x the reference's own fp32 CPU noise where that is
            larger (v11_x). The golden is the reference evaluated in float64.
   bf16/fp16: mean |Δ| (boxes px, scores) <= 2x the reference's own CPU bf16/fp16 forward's
-           mean deviation from the same float64 golden; max |Δ| <= 4x its max.
+           mean deviation from the same float64 golden; box max |Δ| <= 2x its max; class
+           scores: the 99.999th percentile of |Δ| <= 2x its max (at most ~7 of the 672 000
+           scores of an image above it) and the max <= 3x. Measured r03 (max over the
+           reference's max): boxes 0.59-1.22x, scores 0.87-2.16x (n@640 fp16: one score).
 """
+
+
+def half_bars(d, ref_max_box, ref_mean_box, ref_max_cls, ref_mean_cls):
+    """The bf16 / fp16 bar above on |Δ| (N, 4+nc, A) against the reference's own statistics."""
+    box, cls = d[:, :4], d[:, 4:]
+    q = float(np.quantile(np.asarray(cls).ravel(), 0.99999))
+    assert box.mean() <= 2.0 * ref_mean_box and cls.mean() <= 2.0 * ref_mean_cls
+    assert box.max() <= 2.0 * ref_max_box, (float(box.max()), ref_max_box)
+    assert q <= 2.0 * ref_max_cls and cls.max() <= 3.0 * ref_max_cls, (q, float(cls.max()), ref_max_cls)
 import numpy as np
 import pytest
 import torch
@@ -61,8 +73,7 @@ def test_half_precision_within_reference_noise(gpu, dtype, key, variant, size, b
     floor = [float(v) for v in g[key]]
     print(f"v11_{variant}@{size} {dtype}: box max {mine[0]:.3g} mean {mine[1]:.3g} (ref {floor[0]:.3g}/{floor[1]:.3g}); "
           f"cls max {mine[2]:.3g} mean {mine[3]:.3g} (ref {floor[2]:.3g}/{floor[3]:.3g})")
-    assert mine[1] <= 2.0 * floor[1] and mine[3] <= 2.0 * floor[3]
-    assert mine[0] <= 4.0 * floor[0] and mine[2] <= 4.0 * floor[2]
+    half_bars(d.numpy(), floor[0], floor[1], floor[2], floor[3])
 
 
 def test_dropin_module_runs_hip_path(gpu):
@@ -184,8 +195,7 @@ def test_s_fp16_bench_shape(gpu):
     print(f"v11_s@640 fp16 b64: box max {d[:, :4].max():.3g} mean {d[:, :4].mean():.3g} "
           f"(reference fp16 {f[:, :4].max():.3g} / {f[:, :4].mean():.3g}); cls max {d[:, 4:].max():.3g} "
           f"(reference {f[:, 4:].max():.3g})")
-    assert d[:, :4].mean() <= 2 * f[:, :4].mean() and d[:, 4:].mean() <= 2 * f[:, 4:].mean()
-    assert d[:, :4].max() <= 4 * f[:, :4].max() and d[:, 4:].max() <= 4 * f[:, 4:].max()
+    half_bars(d, f[:, :4].max(), f[:, :4].mean(), f[:, 4:].max(), f[:, 4:].mean())
 
 
 def test_x_1280_c5_shape(gpu):
@@ -214,12 +224,41 @@ def test_x_1280_c5_shape(gpu):
     m50, miou = detection_match(dets[0, :counts[0]].cpu().numpy(), want)
     print(f"v11_x@1280 fp32 detections: match@0.5 {m50:.3f} mean IoU {miou:.4f}")
     assert m50 >= 0.99 and miou >= 0.99
-    # bf16 (C5's dtype): within the reference's own bf16 CPU deviation (mean 2x, max 4x)
+    # bf16 (C5's dtype): within the reference's own bf16 CPU deviation (the bar above)
     yb = _engine(model, torch.bfloat16, gpu).forward(x.to(gpu, torch.bfloat16)).float()
     assert torch.isfinite(yb).all()
     d = np.abs(yb[:, :, idx].cpu().double().numpy() - ref)
     fl = [float(v) for v in g["dev_bf16"]]
     print(f"v11_x@1280 bf16: box max {d[:, :4].max():.3g} mean {d[:, :4].mean():.3g} (reference {fl[0]:.3g} / "
           f"{fl[1]:.3g}); cls max {d[:, 4:].max():.3g} mean {d[:, 4:].mean():.3g} (reference {fl[2]:.3g} / {fl[3]:.3g})")
-    assert d[:, :4].mean() <= 2 * fl[1] and d[:, 4:].mean() <= 2 * fl[3]
-    assert d[:, :4].max() <= 4 * fl[0] and d[:, 4:].max() <= 4 * fl[2]
+    half_bars(d, fl[0], fl[1], fl[2], fl[3])
+
+
+def test_x_1280_c5_bench_shape(gpu):
+    """C5's own configuration (v11_x, bf16, 1280x1280, batch 16): the per-shape tuner's plans
+    at batch 16 give every image exactly its batch-1 output (one reduction order for every
+    plan), and image 0 is within the reference's own bf16 deviation of the subsampled float64
+    golden (the bar above, as the batch-1 test)."""
+    from _util import detection_match
+    from yolo_hip.engine import nms
+    g = load_golden("forward_x_1280_b1_sub.npz")
+    idx = torch.from_numpy(g["idx"])
+    ref = g["y_sub"].astype(np.float64)
+    x0 = synth.synth_scenes(1, 1280, 1280, seed=GOLDEN_INPUT_SEED)
+    rest = synth.synth_scenes(15, 1280, 1280, seed=31)
+    x = torch.cat([x0, rest]).to(gpu, torch.bfloat16)
+    eng = _engine(make_model("x"), torch.bfloat16, gpu)
+    y = eng.forward(x).clone()
+    assert torch.isfinite(y.float()).all()
+    for i in (0, 7, 15):
+        y1 = eng.forward(x[i:i + 1].contiguous())
+        assert torch.equal(y1[0], y[i]), f"image {i}: batch-16 plans differ from batch-1"
+    d = np.abs(y[:1, :, idx].float().cpu().double().numpy() - ref)
+    fl = [float(v) for v in g["dev_bf16"]]
+    print(f"v11_x@1280 bf16 b16 image 0: box max {d[:, :4].max():.3g} mean {d[:, :4].mean():.3g} (reference "
+          f"{fl[0]:.3g} / {fl[1]:.3g}); cls max {d[:, 4:].max():.3g} mean {d[:, 4:].mean():.3g}")
+    half_bars(d, fl[0], fl[1], fl[2], fl[3])
+    dets, counts = nms(y[:1])
+    want = g["dets"][:int(g["counts"][0])]
+    m50, miou = detection_match(dets[0, :counts[0]].cpu().numpy(), want)
+    print(f"v11_x@1280 bf16 b16 detections: match@0.5 {m50:.3f} mean IoU {miou:.4f}")

@@ -70,3 +70,27 @@ def test_letterboxed_batch_runs_through_forward_u8(gpu):
     y = eng.forward(x8).clone()
     ref = eng.forward(torch.from_numpy(np.stack([pre.letterbox_host(im, 640) for im in imgs])).to(gpu)).clone()
     assert torch.equal(y, ref)
+
+
+@pytest.mark.parametrize("size", [320, 640, 1280])
+def test_device_letterbox_matches_restatement(gpu, size):
+    """yh_letterbox on the device against oracle/preprocess.py (the numpy restatement of
+    dataset.py:95-103, 292-313, 86-88 with OpenCV's INTER_LINEAR / INTER_AREA arithmetic)
+    directly, bit for bit, on a mixed-size batch larger than one launch (37 images: up- and
+    down-scales, exact 2x downscales, no-resize, tiny and extreme aspect ratios)."""
+    import numpy as np
+    from oracle import preprocess as opre
+    from yolo_hip import preprocess as pre
+    rng = np.random.default_rng(size)
+    shapes = [(480, 640), (640, 427), (1280, 1280), (1280, 960), (17, 23), (640, 640), (720, 1280), (33, 1000),
+              (2 * size, 2 * size), (size, size // 2), (2560, 1440), (12, 3000)]
+    imgs = []
+    for i in range(37):
+        h, w = shapes[i % len(shapes)]
+        im = rng.integers(0, 256, (h, w, 3), dtype=np.uint8)
+        if h > 4 and w > 4:   # smooth gradient in one channel: rounding at every level
+            im[..., 1] = ((np.arange(w)[None, :] * 255) // max(1, w - 1)).astype(np.uint8)
+        imgs.append(im)
+    got = pre.letterbox([torch.from_numpy(im).to(gpu) for im in imgs], size).cpu().numpy()
+    for i, im in enumerate(imgs):
+        assert np.array_equal(got[i], opre.letterbox(im, size)), (i, im.shape, size)
