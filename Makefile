@@ -11,7 +11,7 @@ OBJDIR ?= build/obj
 HIPFLAGS := --offload-arch=$(ARCH) -O3 -fPIC -std=c++17 -Iinclude -I$(SRC) \
             -fhip-fp32-correctly-rounded-divide-sqrt -Wno-unused-result $(EXTRA)
 OBJS := $(OBJDIR)/engine.o $(OBJDIR)/conv.o $(OBJDIR)/misc.o $(OBJDIR)/nms.o $(OBJDIR)/conv_mx.o $(OBJDIR)/nms_host.o \
-        $(OBJDIR)/preprocess.o $(OBJDIR)/head.o $(OBJDIR)/c3k2.o
+        $(OBJDIR)/preprocess.o $(OBJDIR)/head.o $(OBJDIR)/c3k2.o $(OBJDIR)/conv_rw.o
 
 all: $(OUT)
 
@@ -28,6 +28,9 @@ $(OBJDIR)/misc.o: $(SRC)/misc.hip $(SRC)/common.h $(SRC)/dtypes.h | $(OBJDIR)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
 $(OBJDIR)/conv_mx.o: $(SRC)/conv_mx.hip $(SRC)/conv_mx.h $(SRC)/common.h $(SRC)/dtypes.h | $(OBJDIR)
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+$(OBJDIR)/conv_rw.o: $(SRC)/conv_rw.hip $(SRC)/conv_mx.h $(SRC)/common.h $(SRC)/dtypes.h | $(OBJDIR)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
 $(OBJDIR)/nms_host.o: $(SRC)/nms_host.cpp include/yolo_hip.h | $(OBJDIR)

@@ -100,6 +100,8 @@ int main(int argc, char** argv) {
         {"p4.0 3x3s2 128-128 @40", 3, 2, 128, 128, 40, 40, 0, 128, 0, 0},
         {"p4 c3k 3x3 32-32 @40", 3, 1, 32, 32, 40, 40, 0, 32, 0, 0},
         {"h1.res.c1 3x3 64-32 @40", 3, 1, 64, 32, 40, 40, 0, 64, 0, 0},
+        {"h1.res.c2 3x3 32-64 @40 +res", 3, 1, 32, 64, 40, 40, 1, 32, 0, 0},
+        {"p5 c3k.c2 3x3 64-64 @20 +res", 3, 1, 64, 64, 20, 20, 1, 64, 0, 0},
         {"p5.0 3x3s2 128-256 @20", 3, 2, 128, 256, 20, 20, 0, 128, 0, 0},
         {"p5 c3k 3x3 64-64 @20", 3, 1, 64, 64, 20, 20, 0, 64, 0, 0},
         {"h3 3x3s2 64-64 @40", 3, 2, 64, 64, 40, 40, 0, 64, 0, 0},
@@ -128,6 +130,7 @@ int main(int argc, char** argv) {
         sh.ks = L.ks; sh.s = L.s; sh.cin = L.cin; sh.cout = L.cout;
         sh.Ho = L.Ho; sh.Wo = L.Wo; sh.Hi = L.Ho * L.s; sh.Wi = L.Wo * L.s; sh.B = B;
         sh.c0 = L.c1 ? L.c0 : L.cin; sh.c1 = L.c1; sh.up0 = L.c1 ? L.up0 : 0; sh.up1 = 0;
+        sh.ldo = L.cout; sh.ldr = L.res ? L.cout : 0;
         const int hs0 = sh.up0 ? sh.Hi / 2 : sh.Hi, ws0 = sh.up0 ? sh.Wi / 2 : sh.Wi;
         const long long npx0 = (long long)B * hs0 * ws0, npx1 = (long long)B * sh.Hi * sh.Wi;
         const int ldc0 = sh.c0, ldc1 = L.c1 ? L.c1 : 8;
@@ -233,7 +236,7 @@ int main(int argc, char** argv) {
                 }
             }
             printf("  %s na%d mb%d wn%d wm%d ncb%d  task %dx%d bc%d nbi%d ains%d lds%6d grid%5d conf%4d | %8.2f us %7.0f GB/s %6.0f TF | maxd %.3g bad %lld %s\n",
-                   pl.cfg.kind ? "R" : "S", pl.cfg.na, pl.cfg.mb, pl.cfg.wn, pl.cfg.wm, pl.cfg.ncb, pl.TH, pl.TW, 1 << pl.bc_log2, pl.nbi, pl.ains,
+                   pl.cfg.kind == 2 ? (pl.cfg.nbuf == 2 ? "W2" : pl.cfg.nbuf == 3 ? "W3" : "W4") : pl.cfg.kind ? "R" : "S", pl.cfg.na, pl.cfg.mb, pl.cfg.wn, pl.cfg.wm, pl.cfg.ncb, pl.TH, pl.TW, 1 << pl.bc_log2, pl.nbi, pl.ains,
                    pl.lds, pl.grid, pl.conflicts, us, bytes / us * 1e-3, flops / us * 1e-6, maxd, bad,
                    ident ? "ident" : "DIFF");
             if (getenv("MX_TRACE")) {

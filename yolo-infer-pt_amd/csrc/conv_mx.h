@@ -73,12 +73,16 @@ struct MxArgs {
 struct MxConfig {
     int kind = 0;     // 0: conv_mx (staged weights, workgroup-synchronous stages)
                       // 1: conv_mxr (resident weights, per-wave pipelines); wm = waves, wn = 1
+                      // 2: conv_rw (weights in VGPRs, shared patch ring; conv_rw.hip):
+                      //    na = wn = 32-cout groups, wm = pixel groups, tw = tile width,
+                      //    nbuf = patch slots
     int ks, s;        // kernel size (1 / 3), stride (1 / 2)
     int na, mb;       // per wave: na 32-cout A tiles x mb 32-pixel B tiles
     int wn, wm;       // waves along couts x along pixels
     int ncb;          // 16-channel blocks per stage
     int nbi = 0;      // conv_mxr: patch DMA instructions per wave per stage (template)
     int nbuf = 2;     // conv_mxr: patch buffers per wave (1: the next stage's DMA waits for this compute)
+    int tw = 0;       // conv_rw: output tile width (template)
     int bn() const { return 32 * na * wn; }
     int nw() const { return wn * wm; }
 };
@@ -102,7 +106,21 @@ struct MxShape {
     int ks, s, cin, cout, Hi, Wi, Ho, Wo, B;
     int c0, c1;        // segment channel counts (c1 = 0: single segment)
     int up0, up1;
+    int ldo = 0, ldr = 0;   // output / residual pixel strides (0: cout); conv_rw's 32-bit offsets
 };
+
+// conv_rw geometry of a configuration (stride, input channels, cout groups, pixel groups,
+// B tiles per wave, tile width): waves, 16-B chunks per pixel, k-steps, tile pixels and
+// rows, patch rows / cols, DMA instructions per wave per tile, bytes per patch slot
+struct RwGeo {
+    int nw, cpp, nks, tpx, th, pr, pc, nbi, nbr, slot;   // nbr: residual DMA instructions (res)
+};
+RwGeo rw_geo(int S, int cin, int ncg, int npg, int mb, int tw, bool res);
+MxPlan mx_plan_w(const MxShape& sh, const MxConfig& cfg, int num_cus);
+void mx_candidates_w(const MxShape& sh, std::vector<MxConfig>& out);
+std::vector<uint16_t> mx_pack_w(const MxPlan& pl, const MxShape& sh, const float* wf, int cin_logical,
+                                const std::vector<int>& phys2log, bool bf16, int cout_logical);
+int launch_rw(int dtype, const MxPlan& pl, const MxArgs& a, hipStream_t s);
 
 // Candidate configurations for a layer (each with a feasible plan); the first is the
 // heuristic default.

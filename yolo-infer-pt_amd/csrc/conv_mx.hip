@@ -823,6 +823,7 @@ static MxPlan mx_plan_r(const MxShape& sh, const MxConfig& cfg, int num_cus);
 
 MxPlan mx_plan(const MxShape& sh, const MxConfig& cfg, int num_cus) {
     if (cfg.kind == 1) return mx_plan_r(sh, cfg, num_cus);
+    if (cfg.kind == 2) return mx_plan_w(sh, cfg, num_cus);
     MxPlan pl;
     pl.cfg = cfg;
     const MxConfig& c = cfg;
@@ -1026,6 +1027,8 @@ std::vector<MxPlan> mx_candidates(const MxShape& sh, int num_cus) {
                       addr(1, 1, 2, 2); addr(1, 1, 4, 4); }
         else { addr(2, 2, 1, 2); addr(2, 2, 2, 4); addr(2, 2, 4, 8); addr(2, 1, 2, 2); addr(2, 1, 4, 4); }
     }
+    // weights in VGPRs, shared patch ring (conv_rw.hip)
+    mx_candidates_w(sh, cfgs);
     std::vector<MxPlan> out;
     for (auto& c : cfgs) {
         MxPlan p = mx_plan(sh, c, num_cus);
@@ -1037,6 +1040,7 @@ std::vector<MxPlan> mx_candidates(const MxShape& sh, int num_cus) {
 std::vector<uint16_t> mx_pack(const MxPlan& pl, const MxShape& sh, const float* wf, int cin_logical,
                               const std::vector<int>& phys2log, bool bf16, int cout_logical) {
     const MxConfig& c = pl.cfg;
+    if (c.kind == 2) return mx_pack_w(pl, sh, wf, cin_logical, phys2log, bf16, cout_logical);
     if (c.kind == 1) {
         // resident: per slice one image [BN rows][rsw chunks], chunk (cb16*taps + t)*2 + hh
         const int BN = 32 * c.na, NA = c.na, taps = c.ks * c.ks, rsw = pl.nst * c.ncb * taps * 2 + 1;
@@ -1232,6 +1236,7 @@ int launch_mx_dt(const MxPlan& pl, const MxArgs& a, hipStream_t s) {
 
 int launch_mx(int dtype, const MxPlan& pl, const MxArgs& a, hipStream_t s) {
     if (!pl.ok) return (int)hipErrorInvalidValue;
+    if (pl.cfg.kind == 2) return launch_rw(dtype, pl, a, s);
     if (dtype == BF16) return launch_mx_dt<__bf16>(pl, a, s);
     if (dtype == F16) return launch_mx_dt<_Float16>(pl, a, s);
     return (int)hipErrorInvalidValue;

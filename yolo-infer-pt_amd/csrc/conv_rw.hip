@@ -1,0 +1,530 @@
+// conv_rw: the dense 3x3 conv (nets/nn.py:28-39 Conv, s 1 / 2, fused bias + SiLU, the
+// Residual add of nn.py:49) with the layer's weights resident in VGPRs. Kind 2 of the
+// conv_mx plan family: same canonical K order (conv_mx.h), so bit-identical to every
+// other plan of a layer and freely chosen by the per-shape tuner.
+//
+// Why another structure (profiles/r02_conv_ablation.txt): in conv_mx /
+// conv_mxr every wave streams its own patch stage by stage with one stage in flight, and
+// the weights occupy most of the LDS, so patch DMA, MFMA and epilogue ran in series.
+// Here the weights of a wave's 32 couts live in its VGPRs for the whole launch (Cin <= 64:
+// at most 36 k-steps x 4 VGPRs), which frees the whole LDS for a ring of NS patch slots
+// SHARED by the workgroup:
+//   * one persistent workgroup of NW = NCG x NPG waves per CU walks a strided stream of
+//     output tiles (TH x TW pixels of one image, all couts of its slice); wave (cg, pg)
+//     owns cout group cg (32 couts) and MB 32-pixel B tiles of pixel group pg;
+//   * a slot holds a tile's whole input patch (every input channel, full 128-B pixel lines
+//     for Cin = 64), filled by LDS-DMA (global_load_lds_dwordx4) by all waves; the slots
+//     of the next NS-1 tiles are in flight while a tile is multiplied;
+//   * per tile: counted vmcnt (the wave's own DMA of this tile landed; later DMAs and the
+//     previous tiles' stores stay in flight) -> one barrier -> issue the DMA of tile
+//     it + NS - 1 into the slot the previous tile freed -> MFMAs -> epilogue;
+//   * layers with a residual (RES) bring the tile's residual values into the same slot by
+//     LDS-DMA, so the loop issues no VGPR-destination loads at all: hipcc then inserts no
+//     vmcnt wait of its own (a wait for a register load would also drain the patch DMAs
+//     issued before it, in order);
+//   * the epilogue's 16-B stores are buffer instructions issued by every lane for every
+//     pixel (out-of-image pixels get an offset past the buffer's range, which the
+//     hardware drops), so the vmcnt arithmetic is exact.
+#include "conv_mx.h"
+#include "dtypes.h"
+
+#include <algorithm>
+#include <cstring>
+
+namespace yh {
+
+typedef __attribute__((ext_vector_type(16))) float rw_f32x16;
+typedef __attribute__((ext_vector_type(4))) unsigned int rw_u32x4;
+typedef __attribute__((ext_vector_type(2))) float rw_f32x2;
+
+RwGeo rw_geo(int S, int cin, int ncg, int npg, int mb, int tw, bool res) {
+    RwGeo g;
+    g.nw = ncg * npg;
+    g.cpp = cin / 8;
+    g.nks = cin / 16 * 9;
+    g.tpx = npg * mb * 32;
+    g.th = g.tpx / tw;
+    g.pr = S * (g.th - 1) + 3;
+    g.pc = S * (tw - 1) + 3;
+    g.nbi = (g.pr * g.pc * g.cpp + 64 * g.nw - 1) / (64 * g.nw);
+    g.nbr = res ? (g.tpx * ncg * 4 + 64 * g.nw - 1) / (64 * g.nw) : 0;
+    g.slot = (g.nbi + g.nbr) * g.nw * 1024;
+    return g;
+}
+
+namespace {
+
+constexpr unsigned RW_OOB = 0x7ffffff0u;         // buffer offset past every valid byte: dropped
+constexpr int RW_NUM_RECORDS = 0x7ffffff0;
+
+__device__ __forceinline__ void rw_glds(const void* src, unsigned lds_addr) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    unsigned keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep) : "v"(src), "s"(lds_addr) : "memory");
+#else
+    (void)src; (void)lds_addr;
+#endif
+}
+
+template <int N>
+__device__ __forceinline__ void rw_vmwait() {
+    static_assert(N >= 0 && N <= 63, "vmcnt is 6 bits");
+    asm volatile("s_waitcnt vmcnt(%0)" :: "n"(N) : "memory");
+}
+
+__device__ __forceinline__ void rw_barrier() {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+}
+
+__device__ __forceinline__ uint32_t rw_fdiv(uint32_t x, FastDiv d) {
+    return (uint32_t)(((uint64_t)__umulhi(x, d.m) + x) >> d.s);
+}
+
+template <typename T> struct RwMfma;
+template <> struct RwMfma<__bf16> {
+    static __device__ __forceinline__ rw_f32x16 step(const uint4& a, const uint4& b, const rw_f32x16& c) {
+        return __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, a), __builtin_bit_cast(bf16x8, b), c, 0,
+                                                       0, 0);
+    }
+};
+template <> struct RwMfma<_Float16> {
+    static __device__ __forceinline__ rw_f32x16 step(const uint4& a, const uint4& b, const rw_f32x16& c) {
+        return __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(f16x8, a), __builtin_bit_cast(f16x8, b), c, 0, 0,
+                                                      0);
+    }
+};
+
+template <typename T> struct RwPk2;
+template <> struct RwPk2<__bf16> { typedef __attribute__((ext_vector_type(2))) __bf16 v2; };
+template <> struct RwPk2<_Float16> { typedef __attribute__((ext_vector_type(2))) _Float16 v2; };
+template <typename T>
+__device__ __forceinline__ unsigned rw_pack2(float a, float b) {
+    return __builtin_bit_cast(unsigned, __builtin_convertvector(rw_f32x2{a, b}, typename RwPk2<T>::v2));
+}
+template <typename T>
+__device__ __forceinline__ float rw_lo(unsigned u) { return (float)__builtin_bit_cast(T, (unsigned short)(u & 0xffffu)); }
+template <typename T>
+__device__ __forceinline__ float rw_hi(unsigned u) { return (float)__builtin_bit_cast(T, (unsigned short)(u >> 16)); }
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rw_rsrc(const void* base) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, RW_NUM_RECORDS, 0x00020000);
+}
+
+}  // namespace
+
+template <typename T, int S, int CIN, int NCG, int NPG, int MB, int TW, int NS, bool RES>
+__global__ __launch_bounds__(64 * NCG * NPG, NCG * NPG >= 8 ? 2 : 1) void conv_rw(const MxArgs p) {
+    constexpr int NW = NCG * NPG;
+    constexpr int CPP = CIN / 8;                 // 16-B chunks per input pixel
+    constexpr int NKS = CIN / 16 * 9;            // k-steps (canonical order: cb, then tap)
+    constexpr int TPX = NPG * MB * 32;
+    constexpr int TH = TPX / TW;
+    constexpr int PR = S * (TH - 1) + 3, PC = S * (TW - 1) + 3;
+    constexpr int NBI = (PR * PC * CPP + 64 * NW - 1) / (64 * NW);
+    constexpr int RCH = NCG * 4;                 // residual chunks per pixel (the slice's couts)
+    constexpr int RSH = NCG == 2 ? 1 : 2;        // residual image swizzle: chunk ^ (px >> RSH)
+    constexpr int NBR = RES ? (TPX * RCH + 64 * NW - 1) / (64 * NW) : 0;
+    constexpr int SLOT = (NBI + NBR) * NW * 1024;
+    static_assert(TPX % TW == 0 && (CPP & (CPP - 1)) == 0 && NS >= 2, "rw geometry");
+    // VMEM ops a wave issues after its DMAs of tile it, still uncounted at the wait of
+    // iteration it: the epilogues (2 stores per B tile) of the NS-1 earlier tiles and the
+    // DMAs of NS-2 tiles
+    constexpr int CNT = (NS - 1) * 2 * MB + (NS - 2) * (NBI + NBR);
+    static_assert(CNT <= 63, "vmcnt range");
+
+    extern __shared__ __attribute__((aligned(1024))) uint4 sm4[];
+    typedef __attribute__((address_space(3))) uint4* lds_p;
+    const unsigned lds0 = (unsigned)(size_t)(lds_p)sm4;
+    const int lane = threadIdx.x & 63;
+    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int cg = wv % NCG, pg = wv / NCG;
+    const int h = lane >> 5, r32 = lane & 31;
+
+    // workgroup -> (cout slice, stream of tiles); the nslices workgroups of one tile are
+    // adjacent (same XCD under round-robin dispatch: the patch's second read hits L2)
+    const int L = xcd_remap(blockIdx.x, gridDim.x);
+    const int wps = gridDim.x / p.nslices;
+    const int lw = L / p.nslices, sl = L - lw * p.nslices;
+    const int ntile = p.ntasks;
+    const int n_it = lw < ntile ? (ntile - lw + wps - 1) / wps : 0;
+    if (n_it == 0) return;   // workgroup-uniform
+
+    const int sw_sh = p.sw_sh, sw_mr = p.sw_mr;
+    auto swz = [&](int prow, int pcol) { return ((pcol >> sw_sh) + prow * sw_mr) & (CPP - 1); };
+
+    // ---- patch fill slots of this lane (tile independent): packed prow | pcol << 8, and
+    //      the byte offset of the source chunk from the tile's tap-(0,0) pixel
+    int fgeo[NBI], foff[NBI];
+#pragma unroll
+    for (int i = 0; i < NBI; ++i) {
+        const int q = (i * NW + wv) * 64 + lane;
+        const int ppix = q / CPP, cs = q & (CPP - 1);
+        const int prow = ppix / PC, pcol = ppix - prow * PC;
+        const int c = cs ^ swz(prow, pcol);
+        fgeo[i] = ppix < PR * PC ? (prow | (pcol << 8)) : -1;
+        foff[i] = (prow * p.Wi + pcol) * p.ldc0 * 2 + c * 16;
+    }
+    // ---- B fragment chunk index per (tap, B tile) in a slot, and the epilogue pixel
+    int bidx[9][MB], pty[MB], ptx[MB];
+#pragma unroll
+    for (int j = 0; j < MB; ++j) {
+        const int px = (pg * MB + j) * 32 + r32;
+        pty[j] = px / TW;
+        ptx[j] = px % TW;
+#pragma unroll
+        for (int t = 0; t < 9; ++t) {
+            const int prow = S * pty[j] + t / 3, pcol = S * ptx[j] + t % 3;
+            bidx[t][j] = (prow * PC + pcol) * CPP + (h ^ swz(prow, pcol));
+        }
+    }
+
+    // ---- residual fill slots: tile pixel, chunk within the slice's couts (stored at
+    //      chunk ^ (px >> RSH) of the pixel's RCH chunks: conflict-free epilogue reads)
+    int rgeo[NBR > 0 ? NBR : 1];
+#pragma unroll
+    for (int i = 0; i < NBR; ++i) {
+        const int q = (i * NW + wv) * 64 + lane;
+        const int px = q / RCH, cs = q & (RCH - 1);
+        rgeo[i] = px < TPX ? ((px << 4) | (cs ^ ((px >> RSH) & (RCH - 1)))) : -1;
+    }
+
+    auto tile_pos = [&](int it, int& n, int& ty0, int& tx0) {
+        const int t = lw + it * wps;
+        const uint32_t b = rw_fdiv((uint32_t)t, p.d_ntw);
+        tx0 = (t - (int)b * p.ntw) * TW;
+        const uint32_t c = rw_fdiv(b, p.d_nth);
+        ty0 = ((int)b - (int)c * p.nth) * TH;
+        n = (int)c;
+    };
+    // DMA of tile `it`'s patch into slot `slot` (zeros past the stream's end, so every
+    // iteration issues the same number of DMAs)
+    auto issue = [&](int it, int slot) {
+        const unsigned sb = lds0 + (unsigned)(slot * SLOT) + (unsigned)wv * 1024u;
+        if (it < n_it) {
+            int n, ty0, tx0;
+            tile_pos(it, n, ty0, tx0);
+            const int gy0 = S * ty0 - 1, gx0 = S * tx0 - 1;
+            const char* base = p.in0 + (((long long)n * p.Hi + gy0) * p.Wi + gx0) * p.ldc0 * 2;
+#pragma unroll
+            for (int i = 0; i < NBI; ++i) {
+                const int g = fgeo[i];
+                const int gy = gy0 + (g & 255), gx = gx0 + ((g >> 8) & 255);
+                const bool ok = g >= 0 && (unsigned)gy < (unsigned)p.Hi && (unsigned)gx < (unsigned)p.Wi;
+                rw_glds(ok ? (const void*)(base + foff[i]) : (const void*)p.zero, sb + (unsigned)(i * NW * 1024));
+            }
+            if constexpr (RES) {
+                const int cbase = (sl * NCG) * 64;   // byte offset of the slice's couts
+#pragma unroll
+                for (int i = 0; i < NBR; ++i) {
+                    const int g = rgeo[i];
+                    const int px = g >> 4, c = g & 15;
+                    const int oy = ty0 + px / TW, ox = tx0 + px % TW;
+                    const bool ok = g >= 0 && oy < p.Ho && ox < p.Wo;
+                    const char* src = p.res + (((long long)n * p.Ho + oy) * p.Wo + ox) * p.ldr * 2 + cbase + c * 16;
+                    rw_glds(ok ? (const void*)src : (const void*)p.zero, sb + (unsigned)((NBI + i) * NW * 1024));
+                }
+            }
+        } else {
+#pragma unroll
+            for (int i = 0; i < NBI + NBR; ++i) rw_glds(p.zero, sb + (unsigned)(i * NW * 1024));
+        }
+    };
+
+    // ---- prologue: the first NS-1 tiles' patches in flight, then the weights and bias
+    for (int k = 0; k < NS - 1; ++k) issue(k, k);
+    const int co0 = (sl * NCG + cg) * 32;
+    uint4 wf[NKS];
+    {
+        const char* wsrc = p.w + ((long long)(sl * NCG + cg) * NKS * 64 + lane) * 16;
+#pragma unroll
+        for (int s = 0; s < NKS; ++s) wf[s] = *reinterpret_cast<const uint4*>(wsrc + (long long)s * 1024);
+    }
+    float bv[16];
+#pragma unroll
+    for (int e = 0; e < 16; e += 4) {
+        const float4 b4 = *reinterpret_cast<const float4*>(p.bias + co0 + 16 * h + e);
+        bv[e] = b4.x; bv[e + 1] = b4.y; bv[e + 2] = b4.z; bv[e + 3] = b4.w;
+    }
+    // the compiler waits for these loads HERE (not at their first use inside the loop,
+    // where its vmcnt(0) would drain the patch ring every iteration)
+#pragma unroll
+    for (int s = 0; s < NKS; ++s) asm volatile("" :: "v"(wf[s].x), "v"(wf[s].y), "v"(wf[s].z), "v"(wf[s].w));
+#pragma unroll
+    for (int e = 0; e < 16; ++e) asm volatile("" :: "v"(bv[e]));
+    rw_vmwait<0>();
+    rw_barrier();
+
+    const __amdgpu_buffer_rsrc_t ro = rw_rsrc(p.out);
+    const bool silu_act = p.act == ACT_SILU;
+    const unsigned co_b = (unsigned)(co0 + 16 * h) * 2u;
+
+    rw_f32x16 acc[MB];
+    for (int it = 0; it < n_it; ++it) {
+        if (it > 0) {
+            rw_vmwait<CNT>();
+            rw_barrier();   // tile it complete in its slot; slot (it - 1) % NS read by every wave
+        }
+        issue(it + NS - 1, (it + NS - 1) % NS);
+
+        // ---- MFMAs: one k-step = one 32x32x16 step per B tile, fragments of step s+1
+        //      read while step s multiplies
+        {
+            const char* Bp = reinterpret_cast<const char*>(sm4) + (it % NS) * SLOT;
+            auto rd = [](const char* q) { return *reinterpret_cast<const uint4*>(__builtin_assume_aligned(q, 16)); };
+            uint4 bf[2][MB];
+            auto load = [&](int s, int buf) {
+                const int cb = s / 9, t = s - (s / 9) * 9;
+#pragma unroll
+                for (int j = 0; j < MB; ++j) bf[buf][j] = rd(Bp + (bidx[t][j] ^ (2 * cb)) * 16);
+            };
+#pragma unroll
+            for (int j = 0; j < MB; ++j)
+#pragma unroll
+                for (int e = 0; e < 16; ++e) acc[j][e] = 0.f;
+            load(0, 0);
+            __builtin_amdgcn_sched_group_barrier(0x100, MB, 0);
+#pragma unroll
+            for (int s = 0; s < NKS; ++s) {
+                if (s + 1 < NKS) load(s + 1, (s + 1) & 1);
+#pragma unroll
+                for (int j = 0; j < MB; ++j) acc[j] = RwMfma<T>::step(wf[s], bf[s & 1][j], acc[j]);
+                if (s + 1 < NKS) __builtin_amdgcn_sched_group_barrier(0x100, MB, 0);
+                __builtin_amdgcn_sched_group_barrier(0x008, MB, 0);
+            }
+        }
+
+        // ---- epilogue: bias, activation, one rounding (the conv output), the residual added
+        //      in fp32 and rounded again (nets/nn.py:49); 2 x 16-B stores per lane and B tile
+        {
+            int n, ty0, tx0;
+            tile_pos(it, n, ty0, tx0);
+#pragma unroll
+            for (int j = 0; j < MB; ++j) {
+                const int oy = ty0 + pty[j], ox = tx0 + ptx[j];
+                const bool ok = oy < p.Ho && ox < p.Wo;
+                const long long m = ((long long)n * p.Ho + oy) * p.Wo + ox;
+                const unsigned oo = ok ? (unsigned)(m * p.ldo * 2) + co_b : RW_OOB;
+                unsigned w[8];
+#pragma unroll
+                for (int e = 0; e < 16; e += 2) {
+                    float x0 = acc[j][e] + bv[e], x1 = acc[j][e + 1] + bv[e + 1];
+                    if (silu_act) {
+                        x0 = silu<T>(x0);
+                        x1 = silu<T>(x1);
+                    }
+                    w[e >> 1] = rw_pack2<T>(x0, x1);
+                }
+                if constexpr (RES) {
+                    const int px = (pg * MB + j) * 32 + r32, f = (px >> RSH) & (RCH - 1);
+                    const char* rb = reinterpret_cast<const char*>(sm4) + (it % NS) * SLOT + NBI * NW * 1024 + px * RCH * 16;
+                    const uint4 r0 = *reinterpret_cast<const uint4*>(rb + ((cg * 4 + 2 * h) ^ f) * 16);
+                    const uint4 r1 = *reinterpret_cast<const uint4*>(rb + ((cg * 4 + 2 * h + 1) ^ f) * 16);
+                    const unsigned rv[8] = {r0.x, r0.y, r0.z, r0.w, r1.x, r1.y, r1.z, r1.w};
+#pragma unroll
+                    for (int q = 0; q < 8; ++q)
+                        w[q] = rw_pack2<T>(rw_lo<T>(w[q]) + rw_lo<T>(rv[q]), rw_hi<T>(w[q]) + rw_hi<T>(rv[q]));
+                }
+                __builtin_amdgcn_raw_buffer_store_b128(rw_u32x4{w[0], w[1], w[2], w[3]}, ro, oo, 0, 0);
+                __builtin_amdgcn_raw_buffer_store_b128(rw_u32x4{w[4], w[5], w[6], w[7]}, ro, oo + 16u, 0, 0);
+            }
+        }
+    }
+}
+
+// ------------------------------------------------------------------ host side
+namespace {
+
+// extra LDS cycles of the B-fragment reads of one wave over a whole tile (ds_read_b128
+// lane groups, 16-B slots of a 256-B bank row), for swizzle f = ((pcol >> sh) + prow mr) & (cpp-1)
+int rw_conflicts(const RwGeo& g, int S, int tw, int mb, int npg, int sh, int mr) {
+    static const int grp[4][16] = {{0, 1, 2, 3, 12, 13, 14, 15, 20, 21, 22, 23, 24, 25, 26, 27},
+                                   {4, 5, 6, 7, 8, 9, 10, 11, 16, 17, 18, 19, 28, 29, 30, 31},
+                                   {32, 33, 34, 35, 44, 45, 46, 47, 52, 53, 54, 55, 56, 57, 58, 59},
+                                   {36, 37, 38, 39, 40, 41, 42, 43, 48, 49, 50, 51, 60, 61, 62, 63}};
+    const int cpp = g.cpp, ncb = cpp / 2;
+    int total = 0;
+    for (int pgi = 0; pgi < npg; ++pgi)
+        for (int j = 0; j < mb; ++j)
+            for (int t = 0; t < 9; ++t)
+                for (int cb = 0; cb < ncb; ++cb)
+                    for (int q = 0; q < 4; ++q) {
+                        int cnt[16] = {0};
+                        long long seen[16][16];
+                        for (int u = 0; u < 16; ++u) {
+                            const int lane = grp[q][u], h = lane >> 5, r = lane & 31;
+                            const int px = (pgi * mb + j) * 32 + r;
+                            const int prow = S * (px / tw) + t / 3, pcol = S * (px % tw) + t % 3;
+                            const int f = ((pcol >> sh) + prow * mr) & (cpp - 1);
+                            const long long a = ((long long)(prow * g.pc + pcol) * cpp + ((2 * cb + h) ^ f)) * 16;
+                            const int slot = (int)((a / 16) & 15);
+                            bool dup = false;
+                            for (int k = 0; k < cnt[slot]; ++k) dup |= seen[slot][k] == a;
+                            if (!dup) seen[slot][cnt[slot]++] = a;
+                        }
+                        int mx = 0;
+                        for (int s = 0; s < 16; ++s) mx = std::max(mx, cnt[s]);
+                        total += mx - 1;
+                    }
+    return total;
+}
+
+}  // namespace
+
+MxPlan mx_plan_w(const MxShape& sh, const MxConfig& c, int num_cus) {
+    MxPlan pl;
+    pl.cfg = c;
+    if (sh.ks != 3 || c.ks != 3 || sh.s != c.s || sh.c1 != 0 || sh.up0 != 0) return pl;
+    if (!(sh.cin == 16 || sh.cin == 32 || sh.cin == 64) || c.ncb * 16 != sh.cin) return pl;
+    const int ncg = c.na, npg = c.wm, bn = 32 * ncg;
+    if (sh.cout % bn) return pl;
+    // 32-bit buffer offsets: every byte the epilogue addresses below 2^31
+    const double M = (double)sh.B * sh.Ho * sh.Wo;
+    const int ldo = sh.ldo > 0 ? sh.ldo : sh.cout, ldr = sh.ldr > 0 ? sh.ldr : sh.cout;
+    if (M * std::max(ldo, ldr) * 2.0 + 64 > (double)RW_NUM_RECORDS) return pl;
+    const bool res = sh.ldr > 0;
+    const RwGeo g = rw_geo(sh.s, sh.cin, ncg, npg, c.mb, c.tw, res);
+    if (g.tpx % c.tw || g.th < 1 || (res && sh.s != 1)) return pl;
+    pl.TW = c.tw; pl.TH = g.th;
+    pl.PR = g.pr; pl.PC = g.pc;
+    pl.bc_log2 = 0;
+    pl.nbi = g.nbi;
+    pl.ains = g.nbr;   // conv_rw: residual DMA instructions per wave and tile
+    pl.nst = 1;
+    pl.nslices = sh.cout / bn;
+    pl.ntw = (sh.Wo + c.tw - 1) / c.tw;
+    pl.nth = (sh.Ho + g.th - 1) / g.th;
+    pl.ntasks = sh.B * pl.ntw * pl.nth;
+    pl.bbytes = g.slot;
+    pl.abytes = 0;
+    pl.lds = c.nbuf * g.slot;
+    if (pl.lds > 160 * 1024) return pl;
+    pl.wstage = pl.nslices * ncg * g.nks * 1024;   // packed weight bytes
+    int best = 1 << 30, bsh = 0, bmr = 0;
+    for (int s2 = 0; s2 <= 4; ++s2)
+        for (int mr = 0; mr < g.cpp; ++mr) {
+            const int cf = rw_conflicts(g, sh.s, c.tw, c.mb, npg, s2, mr);
+            if (cf < best) { best = cf; bsh = s2; bmr = mr; }
+        }
+    pl.sw_sh = bsh; pl.sw_mr = bmr; pl.conflicts = best;
+    // Cin = 64: the weights take ~150 of a lane's VGPRs, one workgroup per CU; Cin <= 32
+    // 4-wave workgroups fit two per CU
+    const int per_cu = std::max(1, std::min((160 * 1024) / pl.lds, sh.cin <= 32 && g.nw == 4 ? 2 : 1));
+    const int wps = std::max(1, std::min(pl.ntasks, per_cu * num_cus / pl.nslices));
+    pl.grid = wps * pl.nslices;
+    pl.ok = true;
+    return pl;
+}
+
+void mx_candidates_w(const MxShape& sh, std::vector<MxConfig>& out) {
+    if (sh.ks != 3 || sh.c1 != 0 || sh.up0 != 0) return;
+    if (!(sh.cin == 16 || sh.cin == 32 || sh.cin == 64) || sh.cout % 32) return;
+    auto add = [&](int ncg, int npg, int mb, int tw, int ns) {
+        MxConfig c{};
+        c.kind = 2; c.ks = 3; c.s = sh.s; c.na = ncg; c.mb = mb; c.wn = ncg; c.wm = npg; c.ncb = sh.cin / 16;
+        c.tw = tw; c.nbuf = ns;
+        out.push_back(c);
+    };
+    const int ncg = sh.cout % 64 == 0 ? 2 : 1;
+    // the instantiated set (launch_rw_cfg)
+    if (sh.s == 1) {
+        if (sh.cin == 64 && ncg == 2) {
+            add(2, 4, 1, 16, 4); add(2, 4, 1, 8, 4); add(2, 2, 1, 8, 4); add(2, 2, 1, 4, 4);
+        } else if (sh.cin == 64 && ncg == 1) {
+            add(1, 8, 1, 16, 3); add(1, 4, 1, 8, 4);
+        } else if (sh.cin == 32 && ncg == 1) {
+            add(1, 4, 1, 8, 4); add(1, 8, 1, 16, 4);
+        } else if (sh.cin == 32 && ncg == 2) {
+            add(2, 2, 1, 8, 4); add(2, 4, 1, 16, 4);
+        }
+    } else if (sh.cin == 64 && ncg == 2) {
+        add(2, 2, 1, 8, 3); add(2, 4, 1, 16, 2);
+    }
+}
+
+std::vector<uint16_t> mx_pack_w(const MxPlan& pl, const MxShape& sh, const float* wf, int cin_logical,
+                                const std::vector<int>& phys2log, bool bf16, int cout_logical) {
+    const int ncg = pl.cfg.na, nks = sh.cin / 16 * 9;
+    std::vector<uint16_t> out((size_t)pl.wstage / 2, 0);
+    for (int sl = 0; sl < pl.nslices; ++sl)
+        for (int g = 0; g < ncg; ++g)
+            for (int s = 0; s < nks; ++s)
+                for (int lane = 0; lane < 64; ++lane) {
+                    const int R = lane & 31, hh = lane >> 5;
+                    // row permutation: lane half h of the accumulator holds couts 16h .. 16h+15
+                    const int co = (sl * ncg + g) * 32 + 16 * ((R >> 2) & 1) + (R & 3) + 4 * (R >> 3);
+                    const int cb = s / 9, tap = s % 9;
+                    for (int e = 0; e < 8; ++e) {
+                        const int ci = cb * 16 + hh * 8 + e;
+                        if (co >= sh.cout || co >= cout_logical || ci >= (int)phys2log.size()) continue;
+                        const int cl = phys2log[ci];
+                        if (cl < 0) continue;
+                        const float v = wf[((size_t)co * cin_logical + cl) * 9 + tap];
+                        uint32_t u;
+                        std::memcpy(&u, &v, 4);
+                        uint16_t hv;
+                        if (bf16) {
+                            hv = ((u & 0x7fffffffu) > 0x7f800000u) ? (uint16_t)((u >> 16) | 0x40)
+                                                                  : (uint16_t)((u + 0x7fffu + ((u >> 16) & 1)) >> 16);
+                        } else {
+                            _Float16 f16 = (_Float16)v;
+                            std::memcpy(&hv, &f16, 2);
+                        }
+                        out[(((size_t)(sl * ncg + g) * nks + s) * 64 + lane) * 8 + e] = hv;
+                    }
+                }
+    return out;
+}
+
+namespace {
+
+template <typename T, int S, int CIN, int NCG, int NPG, int MB, int TW, int NS, bool RES>
+int launch_rw_t(const MxPlan& pl, const MxArgs& a, hipStream_t s) {
+    const RwGeo g = rw_geo(S, CIN, NCG, NPG, MB, TW, RES);
+    if (g.nbi != pl.nbi || NS * g.slot != pl.lds || RES != (a.res != nullptr)) return (int)hipErrorInvalidValue;
+    static bool attr = false;
+    auto k = &conv_rw<T, S, CIN, NCG, NPG, MB, TW, NS, RES>;
+    if (!attr) {
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  160 * 1024);
+        attr = true;
+    }
+    hipLaunchKernelGGL(k, dim3(pl.grid), dim3(64 * NCG * NPG), pl.lds, s, a);
+    return (int)hipGetLastError();
+}
+
+template <typename T>
+int launch_rw_cfg(const MxPlan& pl, const MxArgs& a, hipStream_t s) {
+    const MxConfig& c = pl.cfg;
+#define YH_RW(S_, CIN_, NCG_, NPG_, MB_, TW_, NS_)                                                           \
+    if (c.s == S_ && c.ncb * 16 == CIN_ && c.na == NCG_ && c.wm == NPG_ && c.mb == MB_ && c.tw == TW_ &&     \
+        c.nbuf == NS_) {                                                                                     \
+        if (S_ == 1 && a.res) return launch_rw_t<T, S_, CIN_, NCG_, NPG_, MB_, TW_, NS_, (S_ == 1)>(pl, a, s); \
+        return launch_rw_t<T, S_, CIN_, NCG_, NPG_, MB_, TW_, NS_, false>(pl, a, s);                           \
+    }
+    YH_RW(1, 64, 2, 4, 1, 16, 4)
+    YH_RW(1, 64, 2, 4, 1, 8, 4)
+    YH_RW(1, 64, 2, 2, 1, 8, 4)
+    YH_RW(1, 64, 2, 2, 1, 4, 4)
+    YH_RW(1, 64, 1, 8, 1, 16, 3)
+    YH_RW(1, 64, 1, 4, 1, 8, 4)
+    YH_RW(1, 32, 1, 4, 1, 8, 4)
+    YH_RW(1, 32, 1, 8, 1, 16, 4)
+    YH_RW(1, 32, 2, 2, 1, 8, 4)
+    YH_RW(1, 32, 2, 4, 1, 16, 4)
+    YH_RW(2, 64, 2, 2, 1, 8, 3)
+    YH_RW(2, 64, 2, 4, 1, 16, 2)
+#undef YH_RW
+    return (int)hipErrorInvalidValue;
+}
+
+}  // namespace
+
+int launch_rw(int dtype, const MxPlan& pl, const MxArgs& a, hipStream_t s) {
+    if (dtype == BF16) return launch_rw_cfg<__bf16>(pl, a, s);
+    if (dtype == F16) return launch_rw_cfg<_Float16>(pl, a, s);
+    return (int)hipErrorInvalidValue;
+}
+
+}  // namespace yh

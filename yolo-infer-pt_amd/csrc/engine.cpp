@@ -940,12 +940,16 @@ struct Net {
         sh.ks = a.KH; sh.s = a.stride; sh.cin = a.Cin; sh.cout = a.Cout;
         sh.Hi = a.Hi; sh.Wi = a.Wi; sh.Ho = a.Ho; sh.Wo = a.Wo; sh.B = B;
         sh.c0 = a.c1 ? a.c0 : a.Cin; sh.c1 = a.c1; sh.up0 = a.up0; sh.up1 = a.up1;
+        sh.ldo = a.ldo; sh.ldr = a.res ? a.ldr : 0;
         return sh;
     }
     static std::string mx_name(const MxPlan& p) {
         char b[96];
-        snprintf(b, sizeof(b), "%s_na%d_mb%d_w%dx%d_ncb%d_t%dx%d", p.cfg.kind ? "mxr" : "mx", p.cfg.na, p.cfg.mb, p.cfg.wn,
-                 p.cfg.wm, p.cfg.ncb, p.TH, p.TW);
+        if (p.cfg.kind == 2)
+            snprintf(b, sizeof(b), "rw_g%d_p%d_mb%d_ns%d_t%dx%d", p.cfg.na, p.cfg.wm, p.cfg.mb, p.cfg.nbuf, p.TH, p.TW);
+        else
+            snprintf(b, sizeof(b), "%s_na%d_mb%d_w%dx%d_ncb%d_t%dx%d", p.cfg.kind ? "mxr" : "mx", p.cfg.na, p.cfg.mb,
+                     p.cfg.wn, p.cfg.wm, p.cfg.ncb, p.TH, p.TW);
         return b;
     }
     // packed weights of conv `ci` in the layout of plan `p` (cached per layout)
