@@ -47,7 +47,16 @@ def test_abi_version_and_error_path():
 def test_nms_workspace_bytes():
     from yolo_hip import _lib
     lib = _lib.lib()
-    assert lib.yh_nms_workspace_bytes(2, 80, 8400) == 2 * 8400 * 80 * 8 + 2 * 4 + 2 * 2048 * 4 + 512
+    def al(v):
+        return (v + 255) // 256 * 256
+    # keys | counts | histograms | per image: state (64 B), gathered first batch (4096 keys),
+    # decoded first batch (3 x 4096 x 16 B), triangular IoU mask (64 x 64 x 65 / 2 words)
+    hist = al(2 * 8400 * 80 * 8 + 2 * 4)
+    state = al(hist + 2 * 2048 * 4)
+    gk = al(state + 2 * 64)
+    ents = al(gk + 2 * 4096 * 8)
+    mask = al(ents + 2 * 3 * 4096 * 16)
+    assert lib.yh_nms_workspace_bytes(2, 80, 8400) == mask + 2 * 64 * 64 * 65 // 2 * 8
     assert lib.yh_nms_workspace_bytes(0, 80, 8400) == 0
 
 

@@ -72,6 +72,25 @@ def test_random_cases_vs_oracle(gpu, seed):
     _assert_same(got, want)
 
 
+@pytest.mark.parametrize("case", ["small_max_wh", "huge_boxes"])
+def test_cross_class_overlap_vs_oracle(gpu, case):
+    """Boxes of different classes overlap after the class offset (max_wh below the coordinate
+    range, or boxes wider than max_wh / 2): the same-class shortcut of the IoU mask must not
+    apply, and cross-class suppression must match the oracle."""
+    rng = np.random.default_rng(7 if case == "huge_boxes" else 8)
+    B, A, nc = 2, 2500, 80
+    y = np.empty((B, 4 + nc, A), np.float32)
+    y[:, 0:2] = rng.uniform(0, 640, size=(B, 2, A))
+    y[:, 2:4] = rng.uniform(8, 200, size=(B, 2, A))
+    if case == "huge_boxes":
+        y[:, 2:4, ::97] = rng.uniform(4000, 20000, size=(B, 2, y[:, 2:4, ::97].shape[-1]))
+    y[:, 4:] = (1 / (1 + np.exp(-rng.normal(-5, 2.5, size=(B, nc, A))))).astype(np.float32)
+    max_wh = 40.0 if case == "small_max_wh" else 7680.0
+    for iou in (0.3, 0.65):
+        want = onms.non_max_suppression(y, 0.001, iou, 300, 30000, max_wh=max_wh)
+        _assert_same(_gpu_nms(torch.from_numpy(y), gpu, iou_threshold=iou, max_wh=max_wh), want)
+
+
 def test_empty_and_ragged_batch(gpu):
     y = torch.zeros(3, 84, 500)
     y[:, 2:4] = 20.0

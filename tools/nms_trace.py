@@ -37,26 +37,32 @@ def main():
         nms(y)
     e1.record()
     torch.cuda.synchronize()
-    print(f"nms (emit + image) per batch of {B}: {e0.elapsed_time(e1) / 20 * 1e3:.1f} us (HIP events, back to back)")
+    print(f"nms (zero + emit + gather + prep + mask + finish) per batch of {B}: {e0.elapsed_time(e1) / 20 * 1e3:.1f} us (HIP events, back to back)")
     tr = torch.zeros((B, 16), dtype=torch.int64, device=dev)
     lib().yh_debug_nms_trace(ctypes.c_void_p(tr.data_ptr()))
     nms(y)
     torch.cuda.synchronize()
     lib().yh_debug_nms_trace(None)
     t = tr.cpu()
-    ph = ["hist-scan", "select+gather", "sort", "greedy(batch0)", "rest", "end"]
+    # marks: 0-3 nms_prep (start, start, gathered keys loaded, sorted + decoded), 4-6 nms_finish
+    # (start, first batch resolved, end); 3 -> 4 is nms_mask plus the launch gaps
+    ph = ["-", "load batch", "sort+decode", "mask(+gaps)", "resolve", "outputs+rest"]
     d = (t[:, 1:7] - t[:, 0:6]).double() * 10.0  # 100 MHz ticks -> ns
     print("per-image phase us (mean / max):")
     for i, name in enumerate(ph):
         print(f"  {name:16s} {d[:, i].mean().item() / 1e3:8.2f} {d[:, i].max().item() / 1e3:8.2f}")
     total = (t[:, 6] - t[:, 0]).double() * 10.0 / 1e3
     print(f"  total            {total.mean().item():8.2f} {total.max().item():8.2f}")
-    sb = (t[:, 12:16] - torch.cat((t[:, 3:4], t[:, 12:15]), 1)).double() * 10.0
-    for i, name in enumerate(["sb0 decode", "sb0 kept+pairwise", "sb0 resolve", "sb0 outputs"]):
-        print(f"  {name:16s} {sb[:, i].mean().item() / 1e3:8.2f} {sb[:, i].max().item() / 1e3:8.2f}")
-    print("batches", t[:, 8].tolist()[:8], "processed", t[:, 9].tolist()[:8], "cands", t[:, 11].tolist()[:8])
-    ghz = (t[:, 10] - t[:, 7]).double() / ((t[:, 6] - t[:, 0]).double() * 10.0)
-    print(f"shader clock during nms_image: {ghz.mean().item():.3f} GHz (s_memtime / s_memrealtime)")
+    k = int((t[:, 6] - t[:, 0]).argmax())
+    if t[k, 8] > 0:   # the slowest image continued past the first batch (nms_rest marks 8, 9, 11, 12-15)
+        r = t[k].double()
+        print(f"image {k} continuation us: hist-scan {(r[8] - r[5]) / 100:.2f} gather {(r[9] - r[8]) / 100:.2f} "
+              f"sort {(r[11] - r[9]) / 100:.2f} sb0 decode {(r[12] - r[11]) / 100:.2f} sb0 kept+pairwise "
+              f"{(r[13] - r[12]) / 100:.2f} sb0 resolve {(r[14] - r[13]) / 100:.2f} sb0 out {(r[15] - r[14]) / 100:.2f} "
+              f"rest {(r[6] - r[15]) / 100:.2f}")
+    print("kernel spans us: prep", ((t[:, 3] - t[:, 0]).max().item() * 10 / 1e3),
+          "finish", ((t[:, 6] - t[:, 4]).max().item() * 10 / 1e3),
+          "prep end -> finish start", ((t[:, 4].min() - t[:, 3].max()).item() * 10 / 1e3))
     start = t[:, 0].min()
     print("block start spread us", ((t[:, 0] - start).double() * 10 / 1e3).max().item())
 

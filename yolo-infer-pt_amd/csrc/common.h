@@ -112,6 +112,12 @@ struct NmsArgs {
     unsigned* hist;            // [B][2048] coarse score-bin histogram (zeroed by the launcher)
     int bin_base;              // (fp32 bits >> 16) of the lowest bin
     float* dets; int* ndet;
+    // first-batch scratch of the split greedy (nms.hip): per image a state record, the
+    // decoded entries in score order and the lower-triangular IoU bitmask
+    unsigned long long* state;  // [B][8]
+    unsigned long long* gkeys;  // [B][4096]: the first batch's keys (unordered)
+    float* ents;                // [B][3][4096][4]: offset box, plain box, (area, score, class, -)
+    unsigned long long* mask;   // [B][64 * 64 * 65 / 2] words
 #ifdef YH_ABLATION
     unsigned long long* trace;  // diagnostic builds only: [B][16] phase timestamps (s_memrealtime)
 #endif

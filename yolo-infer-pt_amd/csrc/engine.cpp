@@ -1644,9 +1644,21 @@ int yh_forward_u8(yh_handle* h, const void* x, int batch, int height, int width,
     });
 }
 
+// workspace: candidate keys [B][A*nc] u64 | counts [B] | histograms [B][2048] | the split greedy's
+// first-batch scratch (yh::NmsArgs::state / gkeys / ents / mask), 256-byte aligned sections
+namespace {
+constexpr size_t NMS_STATE_B = 64, NMS_GK_B = 4096 * 8, NMS_ENTS_B = 3 * 4096 * 16, NMS_MASK_B = 64 * 64 * 65 / 2 * 8;
+size_t nms_al(size_t v) { return (v + 255) & ~(size_t)255; }
+size_t nms_off_hist(int B, int nc, int A) { return nms_al((size_t)B * A * nc * 8 + (size_t)B * 4); }
+size_t nms_off_state(int B, int nc, int A) { return nms_al(nms_off_hist(B, nc, A) + (size_t)B * 2048 * 4); }
+size_t nms_off_gk(int B, int nc, int A) { return nms_al(nms_off_state(B, nc, A) + (size_t)B * NMS_STATE_B); }
+size_t nms_off_ents(int B, int nc, int A) { return nms_al(nms_off_gk(B, nc, A) + (size_t)B * NMS_GK_B); }
+size_t nms_off_mask(int B, int nc, int A) { return nms_al(nms_off_ents(B, nc, A) + (size_t)B * NMS_ENTS_B); }
+}  // namespace
+
 size_t yh_nms_workspace_bytes(int batch, int num_classes, int anchors) {
     if (batch <= 0 || num_classes <= 0 || anchors <= 0) return 0;
-    return (size_t)batch * anchors * num_classes * 8 + (size_t)batch * 4 + (size_t)batch * 2048 * 4 + 512;
+    return nms_off_mask(batch, num_classes, anchors) + (size_t)batch * NMS_MASK_B;
 }
 
 #ifdef YH_ABLATION
@@ -1699,7 +1711,11 @@ int yh_nms(int dtype, const void* y, int batch, int num_classes, int anchors, fl
 #endif
         a.keys = (unsigned long long*)workspace;
         a.counts = (int*)((char*)workspace + (size_t)batch * anchors * num_classes * 8);
-        a.hist = (unsigned*)((char*)workspace + (((size_t)batch * anchors * num_classes * 8 + (size_t)batch * 4 + 255) & ~(size_t)255));
+        a.hist = (unsigned*)((char*)workspace + nms_off_hist(batch, num_classes, anchors));
+        a.state = (unsigned long long*)((char*)workspace + nms_off_state(batch, num_classes, anchors));
+        a.gkeys = (unsigned long long*)((char*)workspace + nms_off_gk(batch, num_classes, anchors));
+        a.ents = (float*)((char*)workspace + nms_off_ents(batch, num_classes, anchors));
+        a.mask = (unsigned long long*)((char*)workspace + nms_off_mask(batch, num_classes, anchors));
         {   // lowest bin at the threshold (or 2047 bins below 1.0 for tiny thresholds)
             uint32_t cb;
             std::memcpy(&cb, &a.conf, 4);

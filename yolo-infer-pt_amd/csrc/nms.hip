@@ -16,12 +16,18 @@
 //              becomes a 56-bit key (score bits << 26 | (2^26-1 - pair)); larger
 //              key = earlier in the reference order. Block-scanned, one atomic
 //              per block, plus a 2048-bin score histogram per image.
-//   nms_image  one 1024-thread workgroup per image: repeatedly radix-selects the
-//              next <= 4096 keys (4 x 14-bit digit histograms in LDS), gathers and
-//              bitonic-sorts them in LDS, then runs greedy NMS on 256-key
-//              sub-batches: parallel test against the kept set, a 256x256 IoU
-//              bitmask, and a one-wave sequential resolve. Stops at max_det kept
-//              or max_nms processed, so typical images touch one batch only.
+//   nms_prep   one 1024-thread workgroup per image: the first batch of whole score
+//              bins (<= 4096 keys) gathered and bitonic-sorted in LDS, each entry
+//              decoded once into the workspace.
+//   nms_mask   the first batches' lower-triangular IoU bitmasks, one wave per 64 x 64
+//              tile, the tiles of all images strided over one grid.
+//   nms_finish one workgroup per image: one wave resolves the greedy order from the
+//              mask, 64 entries per step; the kept entries are written in parallel.
+//              Later batches (an image whose first batch keeps < max_det with
+//              candidates left, or a bin > 4096 keys: radix select with 4 x 14-bit
+//              digit histograms) run greedy NMS on 256-key sub-batches in the same
+//              workgroup: parallel test against the kept set, a 256x256 IoU bitmask
+//              and parallel resolve rounds. Stops at max_det kept or max_nms processed.
 #include "common.h"
 #include "dtypes.h"
 
@@ -61,20 +67,23 @@ __device__ __forceinline__ int score_bin(float s, int base) {
 }
 
 // Candidate emit: a block covers 256 anchors (32 chunks of 8 consecutive anchors,
-// one 16-B load per class row) x 8 class groups; thread (chunk, group) scans the
-// group's classes, remembers which (anchor, class) pairs pass in a bitmask, then
-// re-reads only rows with a passing pair (L1/L2 hits) to write their keys. Keys
-// go out unordered (nms_image orders by key; the key carries the pair index).
+// one 16-B load per class row) x 8 class groups; thread (chunk, group) loads the
+// group's class rows once (the first EMIT_KEEP stay in registers), counts the passing
+// (anchor, class) pairs, and after the block scan writes their keys, staged in LDS and
+// written out contiguously (8-byte scattered stores cost more than the reads). Keys go
+// out unordered (nms_prep orders by key; the key carries the pair index).
 constexpr int EMIT_APT = 8;            // anchors per thread (one 16-B chunk)
 constexpr int EMIT_CHUNKS = 32;        // anchor chunks per block
 constexpr int EMIT_GROUPS = 8;         // class groups per block
-constexpr int EMIT_MAXC = 16;          // classes per group covered by the pass mask
+constexpr int EMIT_KEEP = 12;          // class rows per group held in registers (80 classes: 10)
+constexpr int EMIT_LCAP = 4096;        // keys a block stages in LDS before one coalesced write
 
 template <typename T>
 __global__ __launch_bounds__(256) void nms_emit(const NmsArgs p) {
     __shared__ int wtot[4];
     __shared__ int sbase;
     __shared__ unsigned lhist[NBINS];
+    __shared__ unsigned long long lkeys[EMIT_LCAP];   // the block's keys, written out coalesced
     for (int i = threadIdx.x; i < NBINS; i += 256) lhist[i] = 0;
     const int n = blockIdx.y;
     const int chunk = threadIdx.x & (EMIT_CHUNKS - 1), grp = threadIdx.x / EMIT_CHUNKS;
@@ -83,6 +92,7 @@ __global__ __launch_bounds__(256) void nms_emit(const NmsArgs p) {
     const int cpg = (p.nc + EMIT_GROUPS - 1) / EMIT_GROUPS;
     const int c_lo = grp * cpg, c_hi = min(p.nc, c_lo + cpg);
     const T* y = reinterpret_cast<const T*>(p.y) + (long long)n * (4 + p.nc) * p.A;
+    const bool live = a0 < p.A;
     const bool full = a0 + EMIT_APT <= p.A && (p.A % EMIT_APT) == 0;
     auto row = [&](int c, float (&v)[EMIT_APT]) {
         const T* src = y + (long long)(4 + c) * p.A + a0;
@@ -93,20 +103,35 @@ __global__ __launch_bounds__(256) void nms_emit(const NmsArgs p) {
             for (int e = 0; e < EMIT_APT; ++e) v[e] = a0 + e < p.A ? tof(src[e]) : -1.0f;
         }
     };
+    Chunk<T> keep[EMIT_KEEP];
     int cnt = 0;
-    unsigned rows_hit = 0;   // bit i: class c_lo + i has a passing anchor (i < EMIT_MAXC)
-    if (a0 < p.A) {
-#pragma unroll 4
-        for (int c = c_lo; c < c_hi; ++c) {
+    unsigned rows_hit = 0;   // bit i: row c_lo + i has a passing anchor; bit 31: some row past EMIT_KEEP
+    if (live) {
+        if (full) {
+#pragma unroll
+            for (int i = 0; i < EMIT_KEEP; ++i)
+                if (c_lo + i < c_hi) keep[i] = ld_chunk(y + (long long)(4 + c_lo + i) * p.A + a0);
+        }
+#pragma unroll
+        for (int i = 0; i < EMIT_KEEP; ++i) {
+            if (c_lo + i >= c_hi) continue;
+            float v[EMIT_APT];
+            if (full) chunk_to_f(keep[i], v);
+            else row(c_lo + i, v);
+            int k = 0;
+#pragma unroll
+            for (int e = 0; e < EMIT_APT; ++e) k += v[e] > p.conf;
+            cnt += k;
+            if (k) rows_hit |= 1u << i;
+        }
+        for (int c = c_lo + EMIT_KEEP; c < c_hi; ++c) {
             float v[EMIT_APT];
             row(c, v);
             int k = 0;
 #pragma unroll
             for (int e = 0; e < EMIT_APT; ++e) k += v[e] > p.conf;
             cnt += k;
-            const int i = c - c_lo;
-            if (k && i < EMIT_MAXC) rows_hit |= 1u << i;
-            else if (k) rows_hit |= 0x80000000u;   // a class past the mask: rescan those rows
+            if (k) rows_hit |= 0x80000000u;
         }
     }
     int incl = cnt;
@@ -119,37 +144,55 @@ __global__ __launch_bounds__(256) void nms_emit(const NmsArgs p) {
     __syncthreads();
     if (threadIdx.x == 0) sbase = atomicAdd(&p.counts[n], wtot[0] + wtot[1] + wtot[2] + wtot[3]);
     __syncthreads();
-    int off = sbase + incl - cnt;
+    const int btot = wtot[0] + wtot[1] + wtot[2] + wtot[3];
+    const bool staged = btot <= EMIT_LCAP;   // else (rare) each thread writes its keys directly
+    int off = incl - cnt;                     // offset within the block's keys
     for (int w = 0; w < wave; ++w) off += wtot[w];
-    if (cnt) {
-        unsigned long long* keys = p.keys + (long long)n * p.A * p.nc;
-        for (int c = c_lo; c < c_hi; ++c) {
-            const int i = c - c_lo;
-            const bool hit = i < EMIT_MAXC ? (rows_hit >> i) & 1u : (rows_hit >> 31) & 1u;
-            if (!hit) continue;
-            float v[EMIT_APT];
-            row(c, v);
+    unsigned long long* keys = p.keys + (long long)n * p.A * p.nc + sbase;
+    auto put = [&](int c, const float (&v)[EMIT_APT]) {
 #pragma unroll
-            for (int e = 0; e < EMIT_APT; ++e) {
-                if (v[e] > p.conf) {
-                    keys[off++] = make_key(v[e], (unsigned)((a0 + e) * p.nc + c));
-                    atomicAdd(&lhist[score_bin(v[e], p.bin_base)], 1u);
-                }
+        for (int e = 0; e < EMIT_APT; ++e) {
+            if (v[e] > p.conf) {
+                const unsigned long long k = make_key(v[e], (unsigned)((a0 + e) * p.nc + c));
+                if (staged) lkeys[off++] = k;
+                else keys[off++] = k;
+                atomicAdd(&lhist[score_bin(v[e], p.bin_base)], 1u);
             }
         }
+    };
+    if (cnt) {
+#pragma unroll
+        for (int i = 0; i < EMIT_KEEP; ++i) {
+            if (!((rows_hit >> i) & 1u)) continue;
+            float v[EMIT_APT];
+            if (full) chunk_to_f(keep[i], v);
+            else row(c_lo + i, v);
+            put(c_lo + i, v);
+        }
+        if (rows_hit >> 31)
+            for (int c = c_lo + EMIT_KEEP; c < c_hi; ++c) {
+                float v[EMIT_APT];
+                row(c, v);
+                put(c, v);
+            }
     }
     __syncthreads();
+    if (staged)
+        for (int t = threadIdx.x; t < btot; t += 256) keys[t] = lkeys[t];
     unsigned* gh = p.hist + (long long)n * NBINS;
     for (int i = threadIdx.x; i < NBINS; i += 256)
         if (lhist[i]) atomicAdd(&gh[i], lhist[i]);
 }
 
-// Zeroes the per-image candidate counts and score histograms (one launch instead of
-// two memsets).
-__global__ __launch_bounds__(256) void nms_zero(int* counts, unsigned* hist, int B) {
+// Zeroes the per-image candidate counts, score histograms and gather counters (one
+// launch instead of three memsets).
+__global__ __launch_bounds__(256) void nms_zero(int* counts, unsigned* hist, unsigned long long* state, int B) {
     const int i = blockIdx.x * 256 + threadIdx.x;
     if (i < B * NBINS) hist[i] = 0u;
-    if (i < B) counts[i] = 0;
+    if (i < B) {
+        counts[i] = 0;
+        state[(long long)i * 8 + 4] = 0ull;   // gather counter (STW = 8)
+    }
 }
 
 // IoU test "RN(inter / union) > thr" (fp32 division, torchvision contract) without
@@ -207,6 +250,13 @@ struct NmsSmem {
     int nslow;
     float kb[MAXDET][4];
     float karea[MAXDET];
+    float kcls[MAXDET];
+    // plain-coordinate extent of every entry processed so far (finite: no inf / NaN): with
+    // rhi - rlo <= max_wh / 2 boxes of different classes cannot intersect (class offsets)
+    float rlo, rhi;
+    int rfin;
+    float wlo[NMS_T / 64], whi[NMS_T / 64];
+    int wfin[NMS_T / 64];
     unsigned wsum[NMS_T / 64];
     unsigned long long sel_prefix;
     int sel_need, sel_bin, gcount, kept;
@@ -214,6 +264,24 @@ struct NmsSmem {
 
 template <typename T>
 __device__ __forceinline__ float round_t(float v) { return tof(fromf<T>(v)); }
+
+// A sorted key's entry: the box by wh2xy (util.py:76-82) in the input dtype, the same box
+// offset by class * max_wh (util.py:160-161) and its area, the score and the class.
+template <typename T>
+__device__ __forceinline__ void decode_key(const NmsArgs& p, const T* y, unsigned long long key, float (&ob)[4],
+                                           float (&raw)[4], float& area, float& score, float& cls) {
+    const unsigned pair = PMASK - (unsigned)(key & PMASK);
+    const int a = (int)(pair / (unsigned)p.nc), c = (int)(pair - (unsigned)a * p.nc);
+    const float cx = tof(y[a]), cy = tof(y[(long long)p.A + a]);
+    const float w = tof(y[2LL * p.A + a]), h = tof(y[3LL * p.A + a]);
+    raw[0] = round_t<T>(cx - w / 2.0f); raw[1] = round_t<T>(cy - h / 2.0f);
+    raw[2] = round_t<T>(cx + w / 2.0f); raw[3] = round_t<T>(cy + h / 2.0f);
+    const float off = (float)c * p.max_wh;
+    ob[0] = raw[0] + off; ob[1] = raw[1] + off; ob[2] = raw[2] + off; ob[3] = raw[3] + off;
+    area = (ob[2] - ob[0]) * (ob[3] - ob[1]);
+    score = tof(y[(long long)(4 + c) * p.A + a]);
+    cls = (float)c;
+}
 
 
 // Bitonic sort (descending) of bkeys[0, count), count <= CAP, padded with zero
@@ -333,39 +401,56 @@ __device__ void nms_batch(NmsSmem& S, const NmsArgs& p, const T* y, float* dets,
 #define SB_MARK(k) do { if (NMS_TRACE && tid == 0 && sbi == 0) NMS_TRACE[n * 16 + (k)] = __builtin_amdgcn_s_memrealtime(); } while (0)
         for (int s0 = 0; s0 < want && S.kept < p.max_det; s0 += SB) {
             const int ns = min(SB, want - s0);
+            float lo = INFINITY, hi = -INFINITY;
+            bool fin = true;
             if (tid < ns) {
-                const unsigned long long key = S.bkeys[s0 + tid];
-                const unsigned pair = PMASK - (unsigned)(key & PMASK);
-                const int a = (int)(pair / (unsigned)p.nc), c = (int)(pair - (unsigned)a * p.nc);
-                const float cx = tof(y[a]), cy = tof(y[(long long)p.A + a]);
-                const float w = tof(y[2LL * p.A + a]), h = tof(y[3LL * p.A + a]);
-                // wh2xy (util.py:76-82) in the input dtype
-                const float x1 = round_t<T>(cx - w / 2.0f), y1 = round_t<T>(cy - h / 2.0f);
-                const float x2 = round_t<T>(cx + w / 2.0f), y2 = round_t<T>(cy + h / 2.0f);
-                const float off = (float)c * p.max_wh;
-                const float bx1 = x1 + off, by1 = y1 + off, bx2 = x2 + off, by2 = y2 + off;
-                S.sb[tid][0] = bx1; S.sb[tid][1] = by1; S.sb[tid][2] = bx2; S.sb[tid][3] = by2;
-                S.sarea[tid] = (bx2 - bx1) * (by2 - by1);
-                S.sraw[tid][0] = x1; S.sraw[tid][1] = y1; S.sraw[tid][2] = x2; S.sraw[tid][3] = y2;
-                S.sscore[tid] = tof(y[(long long)(4 + c) * p.A + a]);
-                S.scls[tid] = (float)c;
+                float ob[4], raw[4], area, score, cls;
+                decode_key<T>(p, y, S.bkeys[s0 + tid], ob, raw, area, score, cls);
+                S.sb[tid][0] = ob[0]; S.sb[tid][1] = ob[1]; S.sb[tid][2] = ob[2]; S.sb[tid][3] = ob[3];
+                S.sarea[tid] = area;
+                S.sraw[tid][0] = raw[0]; S.sraw[tid][1] = raw[1]; S.sraw[tid][2] = raw[2]; S.sraw[tid][3] = raw[3];
+                S.sscore[tid] = score;
+                S.scls[tid] = cls;
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    fin &= fabsf(raw[k]) < 3.0e38f;
+                    lo = fminf(lo, raw[k]);
+                    hi = fmaxf(hi, raw[k]);
+                }
             }
+#pragma unroll
+            for (int d = 32; d > 0; d >>= 1) {
+                lo = fminf(lo, __shfl_xor(lo, d));
+                hi = fmaxf(hi, __shfl_xor(hi, d));
+            }
+            fin = __ballot(!fin) == 0ull;
+            if (lane == 0) { S.wlo[wave] = lo; S.whi[wave] = hi; S.wfin[wave] = fin; }
             if (tid < SB / 32) S.supp[tid] = 0;
             if (tid == 0) S.nslow = 0;
             __syncthreads();
             SB_MARK(12);
             const int kept0 = S.kept;
+            lo = S.rlo; hi = S.rhi; fin = S.rfin != 0;
+#pragma unroll
+            for (int w = 0; w < NMS_T / 64; ++w) {
+                lo = fminf(lo, S.wlo[w]);
+                hi = fmaxf(hi, S.whi[w]);
+                fin &= S.wfin[w] != 0;
+            }
+            // classes separable over the kept set and this sub-batch: test same-class pairs only
+            const bool sep = fin && p.max_wh > 0.0f && p.max_wh < 3.0e38f && hi - lo <= 0.5f * p.max_wh;
             bool slow = !th.nonneg;
             {   // 2. suppressed by an already-kept box? 4 threads per entry, 4 kept boxes per step
                 const int e = tid >> 2, part = tid & 3;
                 if (e < ns) {
                     const float ex1 = S.sb[e][0], ey1 = S.sb[e][1], ex2 = S.sb[e][2], ey2 = S.sb[e][3], ea = S.sarea[e];
+                    const float ec = S.scls[e];
                     bool sup = false;
                     for (int k0 = 0; k0 < kept0 && !sup; k0 += 16) {
 #pragma unroll
                         for (int u = 0; u < 4; ++u) {
                             const int k = k0 + 4 * u + part;
-                            if (k < kept0)
+                            if (k < kept0 && (!sep || S.kcls[k] == ec))
                                 sup |= iou_fast(S.kb[k][0], S.kb[k][1], S.kb[k][2], S.kb[k][3], S.karea[k],
                                                 ex1, ey1, ex2, ey2, ea, th, slow);
                         }
@@ -378,9 +463,11 @@ __device__ void nms_batch(NmsSmem& S, const NmsArgs& p, const T* y, float* dets,
                 unsigned long long m = 0;
                 if (i < ns && wd * 64 < i) {
                     const float ix1 = S.sb[i][0], iy1 = S.sb[i][1], ix2 = S.sb[i][2], iy2 = S.sb[i][3], ia = S.sarea[i];
+                    const float ic = S.scls[i];
 #pragma unroll 8
                     for (int jj = 0; jj < 64; ++jj) {
                         const int j = wd * 64 + jj;
+                        if (sep && S.scls[j] != ic) continue;
                         const bool hit = iou_fast(ix1, iy1, ix2, iy2, ia, S.sb[j][0], S.sb[j][1], S.sb[j][2], S.sb[j][3],
                                                   S.sarea[j], th, slow);
                         m |= (unsigned long long)hit << jj;
@@ -465,13 +552,17 @@ __device__ void nms_batch(NmsSmem& S, const NmsArgs& p, const T* y, float* dets,
                         S.kb[o][0] = S.sb[tid][0]; S.kb[o][1] = S.sb[tid][1];
                         S.kb[o][2] = S.sb[tid][2]; S.kb[o][3] = S.sb[tid][3];
                         S.karea[o] = S.sarea[tid];
+                        S.kcls[o] = S.scls[tid];
                         float* d = dets + o * 6;
                         d[0] = S.sraw[tid][0]; d[1] = S.sraw[tid][1]; d[2] = S.sraw[tid][2]; d[3] = S.sraw[tid][3];
                         d[4] = S.sscore[tid]; d[5] = S.scls[tid];
                     }
                 }
                 __syncthreads();
-                if (tid == 0) S.kept = kept0 + min(total, budget);
+                if (tid == 0) {
+                    S.kept = kept0 + min(total, budget);
+                    S.rlo = lo; S.rhi = hi; S.rfin = fin;
+                }
             }
             __syncthreads();
             SB_MARK(15);
@@ -481,8 +572,8 @@ __device__ void nms_batch(NmsSmem& S, const NmsArgs& p, const T* y, float* dets,
 
 // Append every key with pred(key) to bkeys (order irrelevant: the batch is sorted
 // next). GU loads per thread are in flight before any is consumed.
-template <typename Pred>
-__device__ __forceinline__ void gather_keys(NmsSmem& S, const unsigned long long* keys, int nall, int tid, int lane,
+template <typename SM, typename Pred>
+__device__ __forceinline__ void gather_keys(SM& S, const unsigned long long* keys, int nall, int tid, int lane,
                                             Pred pred) {
     constexpr int GU = 8;
     for (int i0 = 0; i0 < nall; i0 += NMS_T * GU) {
@@ -512,7 +603,8 @@ __device__ __forceinline__ void gather_keys(NmsSmem& S, const unsigned long long
 }
 
 // block-wide inclusive scan of one value per thread (1024 threads)
-__device__ unsigned block_scan_incl(NmsSmem& S, unsigned v, int lane, int wave) {
+template <typename SM>
+__device__ unsigned block_scan_incl(SM& S, unsigned v, int lane, int wave) {
     unsigned incl = v;
 #pragma unroll
     for (int d = 1; d < 64; d <<= 1) {
@@ -532,25 +624,296 @@ __device__ unsigned block_scan_incl(NmsSmem& S, unsigned v, int lane, int wave) 
         if (NMS_TRACE && tid == 0) NMS_TRACE[n * 16 + (k)] = __builtin_amdgcn_s_memrealtime(); \
     } while (0)
 
-template <typename T>
-__global__ __launch_bounds__(NMS_T) void nms_image(const NmsArgs p) {
-    extern __shared__ __attribute__((aligned(16))) char smem_raw[];
-    NmsSmem& S = *reinterpret_cast<NmsSmem*>(smem_raw);
-    const int n = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const T* y = reinterpret_cast<const T*>(p.y) + (long long)n * (4 + p.nc) * p.A;
-    const unsigned long long* keys = p.keys + (long long)n * p.A * p.nc;
-    float* dets = p.dets + (long long)n * p.max_det * 6;
+// ---- split greedy for the first batch (the only batch on typical images):
+//   nms_prep    one workgroup per image: score-bin selection, gather and sort of the
+//               first batch (as before), then every entry decoded once into the scratch
+//   nms_mask    the batch's lower-triangular IoU bitmask, one wave per 64 x 64 tile (row i,
+//               word w: bit jj <=> j = 64 w + jj < i and IoU > thr), all images in one grid
+//   nms_finish  one workgroup per image: one wave resolves the greedy order 64 entries at a
+//               time from the mask (LDS copy), all threads write the kept entries; later
+//               batches (rare) continue with the single-workgroup path above
+// The first batch no longer waits on one CU's 256-entry sub-batches: the n^2 / 2 pair
+// tests spread over the whole chip.
+constexpr int ENT = CAP;                      // entries of the first batch in the scratch
+constexpr int MASKW = 64 * 64 * 65 / 2;       // triangular mask words for ENT entries
+constexpr int NB_LDS = 19;                    // row blocks of the mask the resolve stages in LDS
+
+__device__ __forceinline__ int tri(int b) { return 32 * b * (b + 1); }   // first word of row block b
+
+// NmsArgs::state per image (8 words): [0] ub (every key < ub is unprocessed), [1] entries of
+// the first batch, [2] score bin to continue from, [3] flags (bit 0: general path, bit 1:
+// nothing left), [4] keys gathered so far (u32, zeroed by nms_zero), [5] keys selected for the
+// first batch, [6] the batch's upper bin, [7] plain-coordinate extent of the batch (nms_prep)
+constexpr int STW = 8;
+
+__device__ __forceinline__ bool sep_of(unsigned long long ext, float max_wh) {
+    const float lo = __uint_as_float((unsigned)ext), hi = __uint_as_float((unsigned)(ext >> 32));
+    return max_wh > 0.0f && max_wh < 3.0e38f && hi - lo <= 0.5f * max_wh;   // false for the NaN pattern
+}
+
+// C[b] = number of candidates in score bins >= b (suffix sums of the emitted histogram)
+template <typename SM>
+__device__ void bin_suffix(SM& S, const NmsArgs& p, int n, int tid, int lane, int wave) {
+    unsigned* C = S.hist;  // C[0..NBINS], C[NBINS] = 0
+    const unsigned* gh = p.hist + (long long)n * NBINS;
+    const int r0 = 2 * tid, r1 = 2 * tid + 1;  // reversed bin index: b = NBINS-1-r
+    const unsigned h0 = gh[NBINS - 1 - r0], h1 = gh[NBINS - 1 - r1];
+    const unsigned incl = block_scan_incl(S, h0 + h1, lane, wave);
+    C[NBINS - 1 - r1] = incl;
+    C[NBINS - 1 - r0] = incl - h1;
+    if (tid == 0) C[NBINS] = 0;
+    __syncthreads();
+}
+
+// The first batch: whole score bins (blo, bin_hi] holding >= 640 keys (or everything left),
+// at most CAP; bcnt = 0 with flags bit 0: one bin alone exceeds CAP, bit 1: nothing to do.
+template <typename SM>
+__device__ void select_first(SM& S, int ktot, int tid, int& blo, int& bin_hi, int& bcnt, int& flags) {
+    const unsigned* C = S.hist;
+    bin_hi = NBINS - 1;
+    bcnt = 0;
+    blo = -1;
+    flags = ktot > 0 ? 0 : 2;
+    while (ktot > 0) {
+        const unsigned c0 = C[bin_hi + 1];
+        const unsigned target = c0 + 640u, cap = c0 + (unsigned)CAP;   // 640: typically one batch of P = 1024
+        if (tid == 0) {  // default: everything that is left fits the minimum batch
+            S.sel_bin = -1;
+            S.sel_need = (int)(C[0] - c0);
+        }
+        __syncthreads();
+        if (C[0] >= target) {
+#pragma unroll
+            for (int e = 0; e < 2; ++e) {
+                const int b = 2 * tid + e;
+                if (b <= bin_hi && C[b + 1] < target && target <= C[b]) {
+                    if (C[b] <= cap) { S.sel_bin = b - 1; S.sel_need = (int)(C[b] - c0); }
+                    else { S.sel_bin = b; S.sel_need = (int)(C[b + 1] - c0); }
+                }
+            }
+        }
+        __syncthreads();
+        blo = S.sel_bin;
+        bcnt = S.sel_need;
+        __syncthreads();
+        if (bcnt == 0) {
+            if (C[0] == c0) { flags = 2; break; }           // every candidate processed
+            if (blo == bin_hi) { flags = 1; break; }        // one bin alone exceeds CAP
+            bin_hi = blo;                                 // skip empty bins
+            if (bin_hi < 0) { flags = 2; break; }
+            continue;
+        }
+        break;
+    }
+}
+
+// Gather of the first batch's keys, GATHER_G workgroups per image over slices of the
+// candidate list (each recomputes the bin selection from the 8 KB histogram); matches are
+// collected in LDS and appended to the image's gather buffer with one atomic per workgroup.
+struct GatherSmem {
+    unsigned hist[NBINS + 1];
+    unsigned long long bkeys[CAP];
+    unsigned wsum[NMS_T / 64];
+    int sel_bin, sel_need, gcount, gbase;
+};
+constexpr int GATHER_G = 8;
+
+__global__ __launch_bounds__(NMS_T) void nms_gather(const NmsArgs p) {
+    __shared__ GatherSmem S;
+    const int n = blockIdx.y, g = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int nall = p.counts[n];
     const int ktot = min(nall, p.max_nms);
-    if (tid == 0) S.kept = 0;
-    NMS_MARK(0);
-    if (NMS_TRACE && tid == 0) NMS_TRACE[n * 16 + 7] = __builtin_amdgcn_s_memtime();
+    if (tid == 0) S.gcount = 0;
+    bin_suffix(S, p, n, tid, lane, wave);
+    int blo, bin_hi, bcnt, flags;
+    select_first(S, ktot, tid, blo, bin_hi, bcnt, flags);
+    unsigned long long* st = p.state + (long long)n * STW;
+    if (g == 0 && tid == 0) {
+        st[2] = (unsigned long long)(long long)blo;
+        st[3] = (unsigned long long)flags;
+        st[5] = (unsigned long long)bcnt;
+        st[6] = (unsigned long long)(long long)bin_hi;
+    }
+    if (bcnt == 0) return;
+    const int per = (nall + gridDim.x - 1) / gridDim.x;
+    const int lo = g * per, cnt = max(0, min(nall, lo + per) - lo);
+    gather_keys(S, p.keys + (long long)n * p.A * p.nc + lo, cnt, tid, lane, [&](unsigned long long k) {
+        const int bb = score_bin(__uint_as_float((unsigned)(k >> PBITS)), p.bin_base);
+        return bb > blo && bb <= bin_hi;
+    });
+    __syncthreads();
+    const int m = min(S.gcount, CAP);
+    if (tid == 0) S.gbase = m ? (int)atomicAdd(reinterpret_cast<unsigned*>(st + 4), (unsigned)m) : 0;
+    __syncthreads();
+    unsigned long long* gk = p.gkeys + (long long)n * CAP;
+    for (int t = tid; t < m; t += NMS_T)
+        if (S.gbase + t < CAP) gk[S.gbase + t] = S.bkeys[t];
+}
 
-    // C[b] = number of candidates in score bins >= b (suffix sums of the emitted histogram)
-    unsigned* C = S.hist;  // C[0..NBINS], C[NBINS] = 0
+// Sort of the gathered first batch (bitonic in LDS), every entry decoded once.
+template <typename T>
+__global__ __launch_bounds__(NMS_T) void nms_prep(const NmsArgs p) {
+    extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+    NmsSmem& S = *reinterpret_cast<NmsSmem*>(smem_raw);
+    const int n = blockIdx.x, tid = threadIdx.x;
+    const T* y = reinterpret_cast<const T*>(p.y) + (long long)n * (4 + p.nc) * p.A;
+    const int nall = p.counts[n];
+    const int ktot = min(nall, p.max_nms);
+    unsigned long long* st = p.state + (long long)n * STW;
+    NMS_MARK(0);
+    NMS_MARK(1);
+    if (NMS_TRACE && tid == 0) NMS_TRACE[n * 16 + 7] = __builtin_amdgcn_s_memtime();
+    const int bcnt = (int)st[5];
+    const int want = min(bcnt, ktot);
+    if (bcnt > 0) {
+        const unsigned long long* gk = p.gkeys + (long long)n * CAP;
+        for (int t = tid; t < bcnt; t += NMS_T) S.bkeys[t] = gk[t];
+        __syncthreads();
+        NMS_MARK(2);
+        sort_batch(S, bcnt, tid);
+    }
+    float4* E = reinterpret_cast<float4*>(p.ents) + (long long)n * 3 * ENT;
+    // class separability: with every plain coordinate of the batch in [lo, hi] and
+    // hi - lo <= max_wh / 2, boxes of different classes (offset by c * max_wh, rounding
+    // monotonic) cannot intersect, so nms_mask tests same-class pairs only (sep_of)
+    float lo = INFINITY, hi = -INFINITY;
+    bool finite = true;
+    for (int t = tid; t < want; t += NMS_T) {
+        float ob[4], raw[4], area, score, cls;
+        decode_key<T>(p, y, S.bkeys[t], ob, raw, area, score, cls);
+        E[t] = make_float4(ob[0], ob[1], ob[2], ob[3]);
+        E[ENT + t] = make_float4(raw[0], raw[1], raw[2], raw[3]);
+        E[2 * ENT + t] = make_float4(area, score, cls, 0.0f);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            finite &= fabsf(raw[k]) < 3.0e38f;   // false for inf and NaN
+            lo = fminf(lo, raw[k]);
+            hi = fmaxf(hi, raw[k]);
+        }
+    }
+    const int lane = tid & 63, wave = tid >> 6;
+#pragma unroll
+    for (int d = 32; d > 0; d >>= 1) {
+        lo = fminf(lo, __shfl_xor(lo, d));
+        hi = fmaxf(hi, __shfl_xor(hi, d));
+    }
+    const bool wfin = __ballot(!finite) == 0ull;
+    __shared__ float wlo[NMS_T / 64], whi[NMS_T / 64];
+    __shared__ int wok[NMS_T / 64];
+    if (lane == 0) { wlo[wave] = lo; whi[wave] = hi; wok[wave] = wfin; }
+    __syncthreads();
+    if (tid == 0) {
+        bool ok = true;
+        for (int w = 0; w < NMS_T / 64; ++w) {
+            lo = fminf(lo, wlo[w]);
+            hi = fmaxf(hi, whi[w]);
+            ok &= wok[w] != 0;
+        }
+        // [7]: the batch's plain-coordinate extent (lo, hi) as float bits, all ones if not finite
+        st[7] = ok ? ((unsigned long long)__float_as_uint(hi) << 32) | __float_as_uint(lo) : ~0ull;
+        st[0] = want > 0 ? S.bkeys[want - 1] : ~0ull;
+        st[1] = (unsigned long long)want;
+        if (want == 0) st[2] = (unsigned long long)(long long)(int)st[6];   // no batch: bin_hi unchanged
+    }
+    NMS_MARK(3);
+}
+
+// One wave per 64 x 64 tile of a triangle (row block rb, word w <= rb); the tiles of every
+// image of the batch are numbered globally and strided over the grid, so one image's large
+// first batch spreads over the whole chip. Lane r holds row entry 64 rb + r; the tile's 64
+// column entries are staged in LDS. A lane tests only the columns that can hit: those of
+// its own class when the image's classes are separable (most pairs: other classes), else all.
+constexpr int MASK_T = 256;
+
+__global__ __launch_bounds__(MASK_T) void nms_mask(const NmsArgs p) {
+    extern __shared__ int pre[];   // [B + 1]: first global tile of image n
+    __shared__ float4 colb[MASK_T / 64][64];
+    __shared__ float cola[MASK_T / 64][64];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    if (wave == 0) {
+        int carry = 0;
+        for (int c0 = 0; c0 < p.B; c0 += 64) {
+            const int n = c0 + lane;
+            int v = 0;
+            if (n < p.B) {
+                const int nb = ((int)p.state[(long long)n * STW + 1] + 63) >> 6;
+                v = nb * (nb + 1) / 2;
+            }
+            int incl = v;
+#pragma unroll
+            for (int d = 1; d < 64; d <<= 1) {
+                const int o = __shfl_up(incl, d);
+                if (lane >= d) incl += o;
+            }
+            if (n < p.B) pre[n + 1] = carry + incl;
+            carry += __shfl(incl, 63);
+        }
+        if (lane == 0) pre[0] = 0;
+    }
+    __syncthreads();
+    const int total = pre[p.B];
+    const IouThr th = make_thr(p.iou);
+    for (int t = blockIdx.x * (MASK_T / 64) + wave; t < total; t += gridDim.x * (MASK_T / 64)) {
+        int lo = 0, hi = p.B - 1;   // image: the last n with pre[n] <= t
+        while (lo < hi) {
+            const int mid = (lo + hi + 1) >> 1;
+            if (pre[mid] <= t) lo = mid;
+            else hi = mid - 1;
+        }
+        const int n = lo, q = t - pre[n];
+        const int want = (int)p.state[(long long)n * STW + 1];
+        const bool sep = sep_of(p.state[(long long)n * STW + 7], p.max_wh);
+        int rb = (int)((sqrtf(8.0f * (float)q + 1.0f) - 1.0f) * 0.5f);
+        while (rb * (rb + 1) / 2 > q) --rb;
+        while ((rb + 1) * (rb + 2) / 2 <= q) ++rb;
+        const int w = q - rb * (rb + 1) / 2;
+        const float4* E = reinterpret_cast<const float4*>(p.ents) + (long long)n * 3 * ENT;
+        const int i = rb * 64 + lane, j = w * 64 + lane;
+        const int ic = min(i, want - 1), jc = min(j, want - 1);
+        const float4 bi = E[ic], xi = E[2 * ENT + ic];
+        const float4 bj = E[jc], xj = E[2 * ENT + jc];
+        colb[wave][lane] = bj;
+        cola[wave][lane] = xj.x;
+        const int jlim = min(i, want) - w * 64;   // columns jj < jlim (j < i, j < want)
+        unsigned long long cm = jlim >= 64 ? ~0ull : (jlim > 0 ? (1ull << jlim) - 1ull : 0ull);
+        if (sep) {
+            const int ci = (int)xi.z, cj = (int)xj.z;
+            unsigned long long same = 0;
+#pragma unroll
+            for (int jj = 0; jj < 64; ++jj) same |= (unsigned long long)(__builtin_amdgcn_readlane(cj, jj) == ci) << jj;
+            cm &= same;
+        }
+        if (i >= want) cm = 0;
+        unsigned long long m = 0;
+        while (cm) {   // the wave runs max-over-lanes candidate columns
+            const int jj = __ffsll((long long)cm) - 1;
+            cm &= cm - 1ull;
+            const float4 b = colb[wave][jj];
+            const float a = cola[wave][jj];
+            bool hit;
+            if (th.nonneg) {
+                bool slow = false;
+                hit = iou_fast(bi.x, bi.y, bi.z, bi.w, xi.x, b.x, b.y, b.z, b.w, a, th, slow);
+                if (slow) hit = iou_above(bi.x, bi.y, bi.z, bi.w, xi.x, b.x, b.y, b.z, b.w, a, th);
+            } else {
+                hit = iou_above(bi.x, bi.y, bi.z, bi.w, xi.x, b.x, b.y, b.z, b.w, a, th);
+            }
+            m |= (unsigned long long)hit << jj;
+        }
+        p.mask[(long long)n * MASKW + tri(rb) + w * 64 + lane] = m;
+    }
+}
+
+// The greedy over the first batch from its mask, then (rarely) the later batches.
+template <typename T>
+__device__ void nms_rest(NmsSmem& S, const NmsArgs& p, const T* y, float* dets, const unsigned long long* keys,
+                         int nall, int ktot, int processed, unsigned long long ub, int bin_hi, bool fallback,
+                         int tid, int lane, int wave) {
+    const int n = blockIdx.x;
+    unsigned* C = S.hist;
     {
         const unsigned* gh = p.hist + (long long)n * NBINS;
-        const int r0 = 2 * tid, r1 = 2 * tid + 1;  // reversed bin index: b = NBINS-1-r
+        const int r0 = 2 * tid, r1 = 2 * tid + 1;
         const unsigned h0 = gh[NBINS - 1 - r0], h1 = gh[NBINS - 1 - r1];
         const unsigned incl = block_scan_incl(S, h0 + h1, lane, wave);
         C[NBINS - 1 - r1] = incl;
@@ -558,18 +921,13 @@ __global__ __launch_bounds__(NMS_T) void nms_image(const NmsArgs p) {
         if (tid == 0) C[NBINS] = 0;
     }
     __syncthreads();
-    NMS_MARK(1);
-    int nbatch = 0;
-
-    int processed = 0;
-    unsigned long long ub = ~0ull;  // every key < ub is still unprocessed
+    NMS_MARK(8);
+    int nb2 = 0;
     // ---- fast path: batches of whole score bins, ~1024..CAP keys, exact order by an LDS sort
-    int bin_hi = NBINS - 1;
-    bool fallback = false;
-    while (processed < ktot && S.kept < p.max_det && bin_hi >= 0) {
+    while (!fallback && processed < ktot && S.kept < p.max_det && bin_hi >= 0) {
         const unsigned c0 = C[bin_hi + 1];
-        const unsigned target = c0 + 640u, cap = c0 + (unsigned)CAP;   // 640: typically one batch of P = 1024
-        if (tid == 0) {  // default: everything that is left fits the minimum batch
+        const unsigned target = c0 + 640u, cap = c0 + (unsigned)CAP;
+        if (tid == 0) {
             S.sel_bin = -1;
             S.sel_need = (int)(C[0] - c0);
         }
@@ -600,20 +958,17 @@ __global__ __launch_bounds__(NMS_T) void nms_image(const NmsArgs p) {
             return bb > blo && bb <= bin_hi;
         });
         __syncthreads();
-        if (nbatch == 0) NMS_MARK(2);
+        if (nb2 == 0) NMS_MARK(9);
         const int want = min(bcnt, ktot - processed);
         sort_batch(S, bcnt, tid);
-        if (nbatch == 0) NMS_MARK(3);
+        if (nb2 == 0) NMS_MARK(11);
         nms_batch<T>(S, p, y, dets, want, tid, lane, wave);
-        if (nbatch == 0) NMS_MARK(4);
-        ++nbatch;
         processed += want;
         ub = S.bkeys[want - 1];
         bin_hi = blo;
+        ++nb2;
         __syncthreads();
     }
-    NMS_MARK(5);
-    if (NMS_TRACE && tid == 0) { NMS_TRACE[n * 16 + 8] = nbatch; NMS_TRACE[n * 16 + 9] = processed; NMS_TRACE[n * 16 + 11] = nall; }
     if (fallback) {
         // ---- general path: radix-select the next <= CAP keys below ub (exact for any ties)
         while (processed < ktot && S.kept < p.max_det) {
@@ -690,6 +1045,117 @@ __global__ __launch_bounds__(NMS_T) void nms_image(const NmsArgs p) {
             __syncthreads();
         }
     }
+}
+
+template <typename T>
+__global__ __launch_bounds__(NMS_T) void nms_finish(const NmsArgs p) {
+    extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+    NmsSmem& S = *reinterpret_cast<NmsSmem*>(smem_raw);
+    __shared__ unsigned long long Kw[64];   // kept entries of row block b (bit r = entry 64 b + r)
+    __shared__ int Kpre[65];                // kept entries before block b
+    __shared__ int nbd_s;
+    const int n = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const T* y = reinterpret_cast<const T*>(p.y) + (long long)n * (4 + p.nc) * p.A;
+    const unsigned long long* keys = p.keys + (long long)n * p.A * p.nc;
+    float* dets = p.dets + (long long)n * p.max_det * 6;
+    const int nall = p.counts[n];
+    const int ktot = min(nall, p.max_nms);
+    const unsigned long long* st = p.state + (long long)n * STW;
+    const unsigned long long ub = st[0];
+    const int want = (int)st[1], bin_hi = (int)(long long)st[2], flags = (int)st[3];
+    NMS_MARK(4);
+    if (tid == 0) {
+        S.kept = 0;
+        const unsigned long long ext = want > 0 ? st[7] : 0xff800000'7f800000ull;   // (+inf, -inf): empty
+        S.rlo = __uint_as_float((unsigned)ext);
+        S.rhi = __uint_as_float((unsigned)(ext >> 32));
+        S.rfin = ext != ~0ull;
+    }
+    if (want > 0) {
+        // the mask's first NB_LDS row blocks into LDS (over the histogram and key areas, unused
+        // until a later batch), the rest read from the scratch
+        unsigned long long* ML = reinterpret_cast<unsigned long long*>(smem_raw);
+        static_assert(64 * NB_LDS * (NB_LDS + 1) / 2 * 8 <= offsetof(NmsSmem, sb), "mask LDS overlay too large");
+        const unsigned long long* MG = p.mask + (long long)n * MASKW;
+        const int nb = (want + 63) >> 6, nbl = min(nb, NB_LDS);
+        for (int x = tid; x < tri(nbl); x += NMS_T) ML[x] = MG[x];
+        __syncthreads();
+        if (wave == 0) {
+            // block b: entry i = 64 b + r is suppressed by a kept entry of an earlier block (its
+            // row's words w < b against Kw[w]) or of this block (its diagonal word, resolved in
+            // order; entries without an in-block suppressor are decided at once)
+            int kacc = 0, nbd = nb;
+            for (int b = 0; b < nb; ++b) {
+                const int i = b * 64 + lane;
+                const bool valid = i < want;
+                bool sup = false;
+                unsigned long long diag = 0;
+                if (valid) {
+                    unsigned long long acc = 0;
+                    if (b < NB_LDS) {
+                        const unsigned long long* src = ML + tri(b) + lane;
+#pragma unroll 8
+                        for (int w = 0; w < b; ++w) acc |= src[w * 64] & Kw[w];
+                        diag = src[b * 64];
+                    } else {
+                        const unsigned long long* src = MG + tri(b) + lane;
+#pragma unroll 8
+                        for (int w = 0; w < b; ++w) acc |= src[w * 64] & Kw[w];
+                        diag = src[b * 64];
+                    }
+                    sup = acc != 0ull;
+                }
+                const unsigned long long vm = __ballot(valid), sm = __ballot(sup), dm = __ballot(diag != 0ull);
+                unsigned long long kb = vm & ~sm & ~dm, todo = vm & ~sm & dm;
+                const unsigned dlo = (unsigned)diag, dhi = (unsigned)(diag >> 32);
+                while (todo) {
+                    const int r = __ffsll((long long)todo) - 1;
+                    // (readlane returns int: widen through unsigned, not by sign extension)
+                    const unsigned long long d = (unsigned long long)(unsigned)__builtin_amdgcn_readlane(dlo, r) |
+                                                 ((unsigned long long)(unsigned)__builtin_amdgcn_readlane(dhi, r) << 32);
+                    if (!(d & kb)) kb |= 1ull << r;
+                    todo &= todo - 1ull;
+                }
+                int c = __popcll(kb);
+                const int need = p.max_det - kacc;
+                if (c >= need) {   // the greedy stops at max_det kept: the first `need` of this block
+                    unsigned long long keep = 0, rest = kb;
+                    for (int k = 0; k < need; ++k) {
+                        keep |= rest & (~rest + 1ull);
+                        rest &= rest - 1ull;
+                    }
+                    kb = keep;
+                    c = need;
+                }
+                if (lane == 0) { Kw[b] = kb; Kpre[b] = kacc; }
+                kacc += c;
+                if (kacc >= p.max_det) { nbd = b + 1; break; }
+            }
+            if (lane == 0) { Kpre[nbd] = kacc; nbd_s = nbd; S.kept = kacc; }
+        }
+        __syncthreads();
+        NMS_MARK(5);
+        const int nbd = nbd_s;
+        const float4* E = reinterpret_cast<const float4*>(p.ents) + (long long)n * 3 * ENT;
+        for (int t = tid; t < want && t < nbd * 64; t += NMS_T) {
+            const int b = t >> 6, r = t & 63;
+            const unsigned long long K = Kw[b];
+            if ((K >> r) & 1ull) {
+                const int o = Kpre[b] + __popcll(K & ((1ull << r) - 1ull));
+                const float4 ob = E[t], raw = E[ENT + t], ax = E[2 * ENT + t];
+                S.kb[o][0] = ob.x; S.kb[o][1] = ob.y; S.kb[o][2] = ob.z; S.kb[o][3] = ob.w;
+                S.karea[o] = ax.x;
+                S.kcls[o] = ax.z;
+                float* d = dets + o * 6;
+                d[0] = raw.x; d[1] = raw.y; d[2] = raw.z; d[3] = raw.w;
+                d[4] = ax.y; d[5] = ax.z;
+            }
+        }
+    }
+    __syncthreads();
+    const bool fallback = (flags & 1) != 0;
+    const bool more = !(flags & 2) && want < ktot && S.kept < p.max_det && (fallback || bin_hi >= 0);
+    if (more) nms_rest<T>(S, p, y, dets, keys, nall, ktot, want, ub, bin_hi, fallback, tid, lane, wave);
     NMS_MARK(6);
     if (NMS_TRACE && tid == 0) NMS_TRACE[n * 16 + 10] = __builtin_amdgcn_s_memtime();
     if (tid == 0) p.ndet[n] = S.kept;
@@ -697,16 +1163,21 @@ __global__ __launch_bounds__(NMS_T) void nms_image(const NmsArgs p) {
 
 template <typename T>
 int launch_nms_t(const NmsArgs& a, hipStream_t s) {
-    hipLaunchKernelGGL(nms_zero, dim3((a.B * NBINS + 255) / 256), dim3(256), 0, s, a.counts, a.hist, a.B);
+    hipLaunchKernelGGL(nms_zero, dim3((a.B * NBINS + 255) / 256), dim3(256), 0, s, a.counts, a.hist, a.state, a.B);
     const int per_block = EMIT_CHUNKS * EMIT_APT;
     hipLaunchKernelGGL((nms_emit<T>), dim3((a.A + per_block - 1) / per_block, a.B), dim3(256), 0, s, a);
     static bool attr = false;
     if (!attr) {
-        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&nms_image<T>),
-                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)sizeof(NmsSmem));
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&nms_prep<T>),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)sizeof(NmsSmem));
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&nms_finish<T>),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)sizeof(NmsSmem));
         attr = true;
     }
-    hipLaunchKernelGGL((nms_image<T>), dim3(a.B), dim3(NMS_T), sizeof(NmsSmem), s, a);
+    hipLaunchKernelGGL(nms_gather, dim3(GATHER_G, a.B), dim3(NMS_T), 0, s, a);
+    hipLaunchKernelGGL((nms_prep<T>), dim3(a.B), dim3(NMS_T), sizeof(NmsSmem), s, a);
+    hipLaunchKernelGGL(nms_mask, dim3(std::min(2048, 16 * a.B)), dim3(MASK_T), (a.B + 1) * sizeof(int), s, a);
+    hipLaunchKernelGGL((nms_finish<T>), dim3(a.B), dim3(NMS_T), sizeof(NmsSmem), s, a);
     return (int)hipGetLastError();
 }
 
