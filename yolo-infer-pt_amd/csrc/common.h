@@ -155,7 +155,10 @@ struct HeadClsArgs {
     const void* const* io; int A;
 };
 constexpr int HEAD_CLS_THREADS = 256;
-constexpr int HEAD_CLS_LDS = 80 * 1024;    // two workgroups (8 waves) per CU: 8x16 tiles at 80x80
+#ifndef YH_HEAD_CLS_LDS_KB
+#define YH_HEAD_CLS_LDS_KB 80
+#endif
+constexpr int HEAD_CLS_LDS = YH_HEAD_CLS_LDS_KB * 1024;   // 80: two workgroups (8 waves) per CU, 8x16 tiles at 80x80
 // LDS bytes of a tile's buffers; 0 if it does not fit
 int head_cls_lds(int TH, int TW, int C0, int c3, int nc);
 int launch_head_cls(int dtype, const HeadClsArgs& a, hipStream_t s);
