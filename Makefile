@@ -18,7 +18,7 @@ all: $(OUT)
 $(OBJDIR):
 	mkdir -p $(OBJDIR)
 
-$(OBJDIR)/engine.o: $(SRC)/engine.cpp $(SRC)/common.h include/yolo_hip.h | $(OBJDIR)
+$(OBJDIR)/engine.o: $(SRC)/engine.cpp $(SRC)/common.h $(SRC)/conv_mx.h include/yolo_hip.h | $(OBJDIR)
 	$(HIPCC) $(HIPFLAGS) -x hip -c $< -o $@
 
 $(OBJDIR)/conv.o: $(SRC)/conv.hip $(SRC)/common.h $(SRC)/dtypes.h | $(OBJDIR)

@@ -12,6 +12,10 @@
 //   the input channels are cut into 16-channel blocks cb (channels past Cin are
 //   zero); the K walk is  for cb: for tap (kh, kw) row-major:  one 32x32x16 MFMA
 //   step accumulating W[co][cb*16 .. +16][tap] . X[cb*16 .. +16][tap-shifted pixel].
+// K-split layers (mx_kchunks > 1: 3x3 convs with 128 / 256 input channels on maps of at
+// most 40 x 40): the walk is cut into 64-channel chunks, each chunk's partial sum runs the
+// order above from zero, and the partials are added in chunk order (((P0 + P1) + P2) + P3)
+// in fp32 before the bias. Every plan of such a layer (conv_rw kinds only) follows it.
 #pragma once
 #include <stdint.h>
 #include <vector>
@@ -83,6 +87,8 @@ struct MxConfig {
     int nbi = 0;      // conv_mxr: patch DMA instructions per wave per stage (template)
     int nbuf = 2;     // conv_mxr: patch buffers per wave (1: the next stage's DMA waits for this compute)
     int tw = 0;       // conv_rw: output tile width (template)
+    int gdiv = 1;     // conv_rw: workgroups = (one per CU share) / gdiv (fewer weight-image loads)
+    int nkc = 1;      // conv_rw: 64-channel K chunks, one wave each (mx_kchunks of the layer)
     int bn() const { return 32 * na * wn; }
     int nw() const { return wn * wm; }
 };
@@ -114,8 +120,18 @@ struct MxShape {
 // rows, patch rows / cols, DMA instructions per wave per tile, bytes per patch slot
 struct RwGeo {
     int nw, cpp, nks, tpx, th, pr, pc, nbi, nbr, slot;   // nbr: residual DMA instructions (res)
+    int red;                                             // LDS bytes of the K-chunk partials
 };
-RwGeo rw_geo(int S, int cin, int ncg, int npg, int mb, int tw, bool res);
+RwGeo rw_geo(int S, int cin, int ncg, int npg, int mb, int tw, bool res, int nkc);
+// K chunks of a layer's canonical order (1: the plain walk). Shape-dependent (kernel,
+// stride, channels, output map) but batch-independent, so a batch-N forward equals N
+// batch-1 forwards whatever plans the tuner picks.
+inline int mx_kchunks(const MxShape& sh) {
+    if (sh.ks != 3 || sh.c1 != 0 || sh.up0 != 0 || sh.cout % 64 || (long long)sh.Ho * sh.Wo > 1600) return 1;
+    if (sh.s == 1 && (sh.cin == 128 || sh.cin == 256)) return sh.cin / 64;
+    if (sh.s == 2 && sh.cin == 128) return 2;
+    return 1;
+}
 MxPlan mx_plan_w(const MxShape& sh, const MxConfig& cfg, int num_cus);
 void mx_candidates_w(const MxShape& sh, std::vector<MxConfig>& out);
 std::vector<uint16_t> mx_pack_w(const MxPlan& pl, const MxShape& sh, const float* wf, int cin_logical,

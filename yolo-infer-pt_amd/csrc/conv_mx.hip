@@ -822,8 +822,14 @@ int simulate_conflicts(const MxPlan& pl, int sh, int mr) {
 static MxPlan mx_plan_r(const MxShape& sh, const MxConfig& cfg, int num_cus);
 
 MxPlan mx_plan(const MxShape& sh, const MxConfig& cfg, int num_cus) {
-    if (cfg.kind == 1) return mx_plan_r(sh, cfg, num_cus);
     if (cfg.kind == 2) return mx_plan_w(sh, cfg, num_cus);
+    // K-split layers follow the chunked order, which only the conv_rw kernels implement
+    if (mx_kchunks(sh) > 1) {
+        MxPlan none;
+        none.cfg = cfg;
+        return none;
+    }
+    if (cfg.kind == 1) return mx_plan_r(sh, cfg, num_cus);
     MxPlan pl;
     pl.cfg = cfg;
     const MxConfig& c = cfg;

@@ -37,11 +37,11 @@ typedef __attribute__((ext_vector_type(16))) float rw_f32x16;
 typedef __attribute__((ext_vector_type(4))) unsigned int rw_u32x4;
 typedef __attribute__((ext_vector_type(2))) float rw_f32x2;
 
-RwGeo rw_geo(int S, int cin, int ncg, int npg, int mb, int tw, bool res) {
+RwGeo rw_geo(int S, int cin, int ncg, int npg, int mb, int tw, bool res, int nkc) {
     RwGeo g;
-    g.nw = ncg * npg;
+    g.nw = ncg * nkc * npg;
     g.cpp = cin / 8;
-    g.nks = cin / 16 * 9;
+    g.nks = cin / 16 * 9;   // the whole K walk (the packed image); a wave runs nks / nkc steps
     g.tpx = npg * mb * 32;
     g.th = g.tpx / tw;
     g.pr = S * (g.th - 1) + 3;
@@ -49,8 +49,20 @@ RwGeo rw_geo(int S, int cin, int ncg, int npg, int mb, int tw, bool res) {
     g.nbi = (g.pr * g.pc * g.cpp + 64 * g.nw - 1) / (64 * g.nw);
     g.nbr = res ? (g.tpx * ncg * 4 + 64 * g.nw - 1) / (64 * g.nw) : 0;
     g.slot = (g.nbi + g.nbr) * g.nw * 1024;
+    g.red = (nkc - 1) * ncg * npg * mb * 4096;
     return g;
 }
+
+// ablation switches of the micro benchmark (tools/micro, -DYH_ABLATION); off in the shipped
+// library: dbg 4 no MFMA, 8 no epilogue; trace = per-workgroup stamps (entry, prologue done,
+// first tile done, exit)
+#ifdef YH_ABLATION
+#define RW_DBG(bit) (p.dbg & (bit))
+#define RW_TRACE (p.trace)
+#else
+#define RW_DBG(bit) 0
+#define RW_TRACE ((unsigned long long*)nullptr)
+#endif
 
 namespace {
 
@@ -114,32 +126,36 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t rw_rsrc(const void* base) {
 
 }  // namespace
 
-template <typename T, int S, int CIN, int NCG, int NPG, int MB, int TW, int NS, bool RES>
-__global__ __launch_bounds__(64 * NCG * NPG, NCG * NPG >= 8 ? 2 : 1) void conv_rw(const MxArgs p) {
-    constexpr int NW = NCG * NPG;
+template <typename T, int S, int CIN, int NCG, int NPG, int MB, int TW, int NS, bool RES, int NKC>
+__global__ __launch_bounds__(64 * NCG * NKC * NPG, NCG * NKC * NPG >= 8 ? 2 : 1) void conv_rw(const MxArgs p) {
+    constexpr int NW = NCG * NKC * NPG;
     constexpr int CPP = CIN / 8;                 // 16-B chunks per input pixel
-    constexpr int NKS = CIN / 16 * 9;            // k-steps (canonical order: cb, then tap)
+    constexpr int NKT = CIN / 16 * 9;            // k-steps of the whole walk (canonical: cb, then tap)
+    constexpr int NKS = NKT / NKC;               // k-steps of a wave's K chunk
+    constexpr int CBC = CIN / 16 / NKC;          // 16-channel blocks per K chunk
     constexpr int TPX = NPG * MB * 32;
     constexpr int TH = TPX / TW;
     constexpr int PR = S * (TH - 1) + 3, PC = S * (TW - 1) + 3;
     constexpr int NBI = (PR * PC * CPP + 64 * NW - 1) / (64 * NW);
     constexpr int RCH = NCG * 4;                 // residual chunks per pixel (the slice's couts)
-    constexpr int RSH = NCG == 2 ? 1 : 2;        // residual image swizzle: chunk ^ (px >> RSH)
+    constexpr int RSH = NCG == 1 ? 2 : NCG == 2 ? 1 : 0;   // residual image swizzle: chunk ^ (px >> RSH)
     constexpr int NBR = RES ? (TPX * RCH + 64 * NW - 1) / (64 * NW) : 0;
     constexpr int SLOT = (NBI + NBR) * NW * 1024;
-    static_assert(TPX % TW == 0 && (CPP & (CPP - 1)) == 0 && NS >= 2, "rw geometry");
+    static_assert(TPX % TW == 0 && (CPP & (CPP - 1)) == 0 && NS >= 2 && NKT % NKC == 0, "rw geometry");
     // VMEM ops a wave issues after its DMAs of tile it, still uncounted at the wait of
-    // iteration it: the epilogues (2 stores per B tile) of the NS-1 earlier tiles and the
-    // DMAs of NS-2 tiles
-    constexpr int CNT = (NS - 1) * 2 * MB + (NS - 2) * (NBI + NBR);
-    static_assert(CNT <= 63, "vmcnt range");
+    // iteration it: the epilogues (2 stores per B tile; only the chunk-0 waves store) of the
+    // NS-1 earlier tiles and the DMAs of NS-2 tiles
+    constexpr int CNT0 = (NS - 1) * 2 * MB + (NS - 2) * (NBI + NBR);
+    constexpr int CNT1 = (NS - 2) * (NBI + NBR);
+    static_assert(CNT0 <= 63, "vmcnt range");
 
+    const unsigned long long t_entry = RW_TRACE ? __builtin_amdgcn_s_memrealtime() : 0ull;
     extern __shared__ __attribute__((aligned(1024))) uint4 sm4[];
     typedef __attribute__((address_space(3))) uint4* lds_p;
     const unsigned lds0 = (unsigned)(size_t)(lds_p)sm4;
     const int lane = threadIdx.x & 63;
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int cg = wv % NCG, pg = wv / NCG;
+    const int cg = wv % NCG, kc = (wv / NCG) % NKC, pg = wv / (NCG * NKC);
     const int h = lane >> 5, r32 = lane & 31;
 
     // workgroup -> (cout slice, stream of tiles); the nslices workgroups of one tile are
@@ -176,7 +192,9 @@ __global__ __launch_bounds__(64 * NCG * NPG, NCG * NPG >= 8 ? 2 : 1) void conv_r
 #pragma unroll
         for (int t = 0; t < 9; ++t) {
             const int prow = S * pty[j] + t / 3, pcol = S * ptx[j] + t % 3;
-            bidx[t][j] = (prow * PC + pcol) * CPP + (h ^ swz(prow, pcol));
+            // the wave's K chunk starts at block kc * CBC: its chunk bits are folded in here,
+            // so the k-step loop XORs compile-time block offsets only
+            bidx[t][j] = ((prow * PC + pcol) * CPP + (h ^ swz(prow, pcol))) ^ (2 * kc * CBC);
         }
     }
 
@@ -237,7 +255,7 @@ __global__ __launch_bounds__(64 * NCG * NPG, NCG * NPG >= 8 ? 2 : 1) void conv_r
     const int co0 = (sl * NCG + cg) * 32;
     uint4 wf[NKS];
     {
-        const char* wsrc = p.w + ((long long)(sl * NCG + cg) * NKS * 64 + lane) * 16;
+        const char* wsrc = p.w + ((long long)(sl * NCG + cg) * NKT * 64 + kc * NKS * 64 + lane) * 16;
 #pragma unroll
         for (int s = 0; s < NKS; ++s) wf[s] = *reinterpret_cast<const uint4*>(wsrc + (long long)s * 1024);
     }
@@ -255,6 +273,8 @@ __global__ __launch_bounds__(64 * NCG * NPG, NCG * NPG >= 8 ? 2 : 1) void conv_r
     for (int e = 0; e < 16; ++e) asm volatile("" :: "v"(bv[e]));
     rw_vmwait<0>();
     rw_barrier();
+    const unsigned long long t_setup = RW_TRACE ? __builtin_amdgcn_s_memrealtime() : 0ull;
+    unsigned long long t_first = 0ull;
 
     const __amdgpu_buffer_rsrc_t ro = rw_rsrc(p.out);
     const bool silu_act = p.act == ACT_SILU;
@@ -263,8 +283,10 @@ __global__ __launch_bounds__(64 * NCG * NPG, NCG * NPG >= 8 ? 2 : 1) void conv_r
     rw_f32x16 acc[MB];
     for (int it = 0; it < n_it; ++it) {
         if (it > 0) {
-            rw_vmwait<CNT>();
+            if (kc == 0) rw_vmwait<CNT0>();
+            else rw_vmwait<CNT1>();
             rw_barrier();   // tile it complete in its slot; slot (it - 1) % NS read by every wave
+            if (RW_TRACE && it == 1) t_first = __builtin_amdgcn_s_memrealtime();
         }
         issue(it + NS - 1, (it + NS - 1) % NS);
 
@@ -288,6 +310,7 @@ __global__ __launch_bounds__(64 * NCG * NPG, NCG * NPG >= 8 ? 2 : 1) void conv_r
 #pragma unroll
             for (int s = 0; s < NKS; ++s) {
                 if (s + 1 < NKS) load(s + 1, (s + 1) & 1);
+                if (RW_DBG(4)) continue;
 #pragma unroll
                 for (int j = 0; j < MB; ++j) acc[j] = RwMfma<T>::step(wf[s], bf[s & 1][j], acc[j]);
                 if (s + 1 < NKS) __builtin_amdgcn_sched_group_barrier(0x100, MB, 0);
@@ -295,9 +318,33 @@ __global__ __launch_bounds__(64 * NCG * NPG, NCG * NPG >= 8 ? 2 : 1) void conv_r
             }
         }
 
-        // ---- epilogue: bias, activation, one rounding (the conv output), the residual added
-        //      in fp32 and rounded again (nets/nn.py:49); 2 x 16-B stores per lane and B tile
-        {
+        // ---- K chunks: the partials of chunks 1.. through LDS ([chunk][pg][cg][j][reg][lane]
+        //      floats, lane-consecutive), added by the chunk-0 wave in chunk order
+        if constexpr (NKC > 1) {
+            float* red = reinterpret_cast<float*>(reinterpret_cast<char*>(sm4) + NS * SLOT);
+            auto rslot = [&](int k2, int j) { return red + ((((k2 - 1) * NPG + pg) * NCG + cg) * MB + j) * 1024 + lane; };
+            if (kc > 0) {
+#pragma unroll
+                for (int j = 0; j < MB; ++j)
+#pragma unroll
+                    for (int e = 0; e < 16; ++e) rslot(kc, j)[e * 64] = acc[j][e];
+            }
+            rw_barrier();
+            if (kc == 0) {
+#pragma unroll
+                for (int k2 = 1; k2 < NKC; ++k2) {
+#pragma unroll
+                    for (int j = 0; j < MB; ++j)
+#pragma unroll
+                        for (int e = 0; e < 16; ++e) acc[j][e] += rslot(k2, j)[e * 64];
+                    asm volatile("" ::: "memory");   // one chunk's 16 x MB reads in flight, not all
+                }
+            }
+        }
+        // ---- epilogue (chunk-0 waves): bias, activation, one rounding (the conv output), the
+        //      residual added in fp32 and rounded again (nets/nn.py:49); 2 x 16-B stores per
+        //      lane and B tile
+        if (kc == 0) {
             int n, ty0, tx0;
             tile_pos(it, n, ty0, tx0);
 #pragma unroll
@@ -326,10 +373,15 @@ __global__ __launch_bounds__(64 * NCG * NPG, NCG * NPG >= 8 ? 2 : 1) void conv_r
                     for (int q = 0; q < 8; ++q)
                         w[q] = rw_pack2<T>(rw_lo<T>(w[q]) + rw_lo<T>(rv[q]), rw_hi<T>(w[q]) + rw_hi<T>(rv[q]));
                 }
-                __builtin_amdgcn_raw_buffer_store_b128(rw_u32x4{w[0], w[1], w[2], w[3]}, ro, oo, 0, 0);
-                __builtin_amdgcn_raw_buffer_store_b128(rw_u32x4{w[4], w[5], w[6], w[7]}, ro, oo + 16u, 0, 0);
+                const unsigned od = RW_DBG(8) ? RW_OOB : oo;
+                __builtin_amdgcn_raw_buffer_store_b128(rw_u32x4{w[0], w[1], w[2], w[3]}, ro, od, 0, 0);
+                __builtin_amdgcn_raw_buffer_store_b128(rw_u32x4{w[4], w[5], w[6], w[7]}, ro, od + 16u, 0, 0);
             }
         }
+    }
+    if (RW_TRACE && threadIdx.x == 0) {
+        unsigned long long* tr = RW_TRACE + blockIdx.x * 4;
+        tr[0] = t_entry; tr[1] = t_setup; tr[2] = t_first ? t_first : t_setup; tr[3] = __builtin_amdgcn_s_memrealtime();
     }
 }
 
@@ -376,7 +428,9 @@ MxPlan mx_plan_w(const MxShape& sh, const MxConfig& c, int num_cus) {
     MxPlan pl;
     pl.cfg = c;
     if (sh.ks != 3 || c.ks != 3 || sh.s != c.s || sh.c1 != 0 || sh.up0 != 0) return pl;
-    if (!(sh.cin == 16 || sh.cin == 32 || sh.cin == 64) || c.ncb * 16 != sh.cin) return pl;
+    // a wave keeps 64 input channels' weights (36 k-steps) at most: wider layers are K-split
+    if (c.ncb * 16 != sh.cin || c.nkc != mx_kchunks(sh) || sh.cin / c.nkc > 64) return pl;
+    if (!(sh.cin / c.nkc == 16 || sh.cin / c.nkc == 32 || sh.cin / c.nkc == 64)) return pl;
     const int ncg = c.na, npg = c.wm, bn = 32 * ncg;
     if (sh.cout % bn) return pl;
     // 32-bit buffer offsets: every byte the epilogue addresses below 2^31
@@ -384,7 +438,7 @@ MxPlan mx_plan_w(const MxShape& sh, const MxConfig& c, int num_cus) {
     const int ldo = sh.ldo > 0 ? sh.ldo : sh.cout, ldr = sh.ldr > 0 ? sh.ldr : sh.cout;
     if (M * std::max(ldo, ldr) * 2.0 + 64 > (double)RW_NUM_RECORDS) return pl;
     const bool res = sh.ldr > 0;
-    const RwGeo g = rw_geo(sh.s, sh.cin, ncg, npg, c.mb, c.tw, res);
+    const RwGeo g = rw_geo(sh.s, sh.cin, ncg, npg, c.mb, c.tw, res, c.nkc);
     if (g.tpx % c.tw || g.th < 1 || (res && sh.s != 1)) return pl;
     pl.TW = c.tw; pl.TH = g.th;
     pl.PR = g.pr; pl.PC = g.pc;
@@ -398,8 +452,8 @@ MxPlan mx_plan_w(const MxShape& sh, const MxConfig& c, int num_cus) {
     pl.ntasks = sh.B * pl.ntw * pl.nth;
     pl.bbytes = g.slot;
     pl.abytes = 0;
-    pl.lds = c.nbuf * g.slot;
-    if (pl.lds > 160 * 1024) return pl;
+    pl.lds = c.nbuf * g.slot + g.red;
+    if (pl.lds > 160 * 1024 || g.nw > 16) return pl;
     pl.wstage = pl.nslices * ncg * g.nks * 1024;   // packed weight bytes
     int best = 1 << 30, bsh = 0, bmr = 0;
     for (int s2 = 0; s2 <= 4; ++s2)
@@ -411,24 +465,43 @@ MxPlan mx_plan_w(const MxShape& sh, const MxConfig& c, int num_cus) {
     // Cin = 64: the weights take ~150 of a lane's VGPRs, one workgroup per CU; Cin <= 32
     // 4-wave workgroups fit two per CU
     const int per_cu = std::max(1, std::min((160 * 1024) / pl.lds, sh.cin <= 32 && g.nw == 4 ? 2 : 1));
-    const int wps = std::max(1, std::min(pl.ntasks, per_cu * num_cus / pl.nslices));
+    // every wave loads its cout group's whole weight image: fewer, longer-lived workgroups
+    // (gdiv) trade parallelism for weight traffic on small layers
+    const int wps = std::max(1, std::min(pl.ntasks, per_cu * num_cus / pl.nslices) / std::max(1, c.gdiv));
     pl.grid = wps * pl.nslices;
     pl.ok = true;
     return pl;
 }
 
 void mx_candidates_w(const MxShape& sh, std::vector<MxConfig>& out) {
-    if (sh.ks != 3 || sh.c1 != 0 || sh.up0 != 0) return;
-    if (!(sh.cin == 16 || sh.cin == 32 || sh.cin == 64) || sh.cout % 32) return;
+    if (sh.ks != 3 || sh.c1 != 0 || sh.up0 != 0 || sh.cout % 32) return;
+    const int nkc = mx_kchunks(sh);
+    if (!(sh.cin == 16 || sh.cin == 32 || sh.cin == 64 || nkc > 1)) return;
+    // small layers (fewer tiles than 2 per CU) also get the grid halved and quartered
+    const bool small = (double)sh.B * sh.Ho * sh.Wo < 2.0 * 256 * 64;
     auto add = [&](int ncg, int npg, int mb, int tw, int ns) {
         MxConfig c{};
         c.kind = 2; c.ks = 3; c.s = sh.s; c.na = ncg; c.mb = mb; c.wn = ncg; c.wm = npg; c.ncb = sh.cin / 16;
-        c.tw = tw; c.nbuf = ns;
-        out.push_back(c);
+        c.tw = tw; c.nbuf = ns; c.nkc = nkc;
+        for (int gd : {1, 2, 4}) {
+            if (gd > 1 && !small) break;
+            c.gdiv = gd;
+            out.push_back(c);
+        }
     };
     const int ncg = sh.cout % 64 == 0 ? 2 : 1;
     // the instantiated set (launch_rw_cfg)
-    if (sh.s == 1) {
+    if (nkc > 1) {
+        if (sh.s == 1 && sh.cin == 128) {
+            add(2, 2, 1, 8, 3); add(2, 1, 1, 8, 3); add(2, 1, 1, 8, 4);
+            if (sh.cout % 128 == 0) add(4, 1, 1, 8, 3);
+        } else if (sh.s == 1 && sh.cin == 256) {
+            add(2, 1, 1, 8, 3); add(2, 1, 1, 4, 3);
+        } else if (sh.s == 2 && sh.cin == 128) {
+            add(2, 2, 1, 8, 2); add(2, 1, 1, 8, 3);
+            if (sh.cout % 128 == 0) add(4, 1, 1, 8, 3);
+        }
+    } else if (sh.s == 1) {
         if (sh.cin == 64 && ncg == 2) {
             add(2, 4, 1, 16, 4); add(2, 4, 1, 8, 4); add(2, 2, 1, 8, 4); add(2, 2, 1, 4, 4);
         } else if (sh.cin == 64 && ncg == 1) {
@@ -440,6 +513,8 @@ void mx_candidates_w(const MxShape& sh, std::vector<MxConfig>& out) {
         }
     } else if (sh.cin == 64 && ncg == 2) {
         add(2, 2, 1, 8, 3); add(2, 4, 1, 16, 2);
+        // 128 couts in one workgroup: the patch is read once, not once per 64-cout slice
+        if (sh.cout % 128 == 0) { add(4, 2, 1, 8, 3); add(4, 1, 1, 8, 4); }
     }
 }
 
@@ -479,42 +554,54 @@ std::vector<uint16_t> mx_pack_w(const MxPlan& pl, const MxShape& sh, const float
 
 namespace {
 
-template <typename T, int S, int CIN, int NCG, int NPG, int MB, int TW, int NS, bool RES>
+template <typename T, int S, int CIN, int NCG, int NPG, int MB, int TW, int NS, bool RES, int NKC>
 int launch_rw_t(const MxPlan& pl, const MxArgs& a, hipStream_t s) {
-    const RwGeo g = rw_geo(S, CIN, NCG, NPG, MB, TW, RES);
-    if (g.nbi != pl.nbi || NS * g.slot != pl.lds || RES != (a.res != nullptr)) return (int)hipErrorInvalidValue;
+    const RwGeo g = rw_geo(S, CIN, NCG, NPG, MB, TW, RES, NKC);
+    if (g.nbi != pl.nbi || NS * g.slot + g.red != pl.lds || RES != (a.res != nullptr)) return (int)hipErrorInvalidValue;
     static bool attr = false;
-    auto k = &conv_rw<T, S, CIN, NCG, NPG, MB, TW, NS, RES>;
+    auto k = &conv_rw<T, S, CIN, NCG, NPG, MB, TW, NS, RES, NKC>;
     if (!attr) {
         (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize,
                                   160 * 1024);
         attr = true;
     }
-    hipLaunchKernelGGL(k, dim3(pl.grid), dim3(64 * NCG * NPG), pl.lds, s, a);
+    hipLaunchKernelGGL(k, dim3(pl.grid), dim3(64 * NCG * NKC * NPG), pl.lds, s, a);
     return (int)hipGetLastError();
 }
 
 template <typename T>
 int launch_rw_cfg(const MxPlan& pl, const MxArgs& a, hipStream_t s) {
     const MxConfig& c = pl.cfg;
-#define YH_RW(S_, CIN_, NCG_, NPG_, MB_, TW_, NS_)                                                           \
+#define YH_RW(S_, CIN_, NCG_, NPG_, MB_, TW_, NS_, NKC_)                                                    \
     if (c.s == S_ && c.ncb * 16 == CIN_ && c.na == NCG_ && c.wm == NPG_ && c.mb == MB_ && c.tw == TW_ &&     \
-        c.nbuf == NS_) {                                                                                     \
-        if (S_ == 1 && a.res) return launch_rw_t<T, S_, CIN_, NCG_, NPG_, MB_, TW_, NS_, (S_ == 1)>(pl, a, s); \
-        return launch_rw_t<T, S_, CIN_, NCG_, NPG_, MB_, TW_, NS_, false>(pl, a, s);                           \
+        c.nbuf == NS_ && c.nkc == NKC_) {                                                                    \
+        if (S_ == 1 && a.res) return launch_rw_t<T, S_, CIN_, NCG_, NPG_, MB_, TW_, NS_, (S_ == 1), NKC_>(pl, a, s); \
+        return launch_rw_t<T, S_, CIN_, NCG_, NPG_, MB_, TW_, NS_, false, NKC_>(pl, a, s);                     \
     }
-    YH_RW(1, 64, 2, 4, 1, 16, 4)
-    YH_RW(1, 64, 2, 4, 1, 8, 4)
-    YH_RW(1, 64, 2, 2, 1, 8, 4)
-    YH_RW(1, 64, 2, 2, 1, 4, 4)
-    YH_RW(1, 64, 1, 8, 1, 16, 3)
-    YH_RW(1, 64, 1, 4, 1, 8, 4)
-    YH_RW(1, 32, 1, 4, 1, 8, 4)
-    YH_RW(1, 32, 1, 8, 1, 16, 4)
-    YH_RW(1, 32, 2, 2, 1, 8, 4)
-    YH_RW(1, 32, 2, 4, 1, 16, 4)
-    YH_RW(2, 64, 2, 2, 1, 8, 3)
-    YH_RW(2, 64, 2, 4, 1, 16, 2)
+    YH_RW(1, 64, 2, 4, 1, 16, 4, 1)
+    YH_RW(1, 64, 2, 4, 1, 8, 4, 1)
+    YH_RW(1, 64, 2, 2, 1, 8, 4, 1)
+    YH_RW(1, 64, 2, 2, 1, 4, 4, 1)
+    YH_RW(1, 64, 1, 8, 1, 16, 3, 1)
+    YH_RW(1, 64, 1, 4, 1, 8, 4, 1)
+    YH_RW(1, 32, 1, 4, 1, 8, 4, 1)
+    YH_RW(1, 32, 1, 8, 1, 16, 4, 1)
+    YH_RW(1, 32, 2, 2, 1, 8, 4, 1)
+    YH_RW(1, 32, 2, 4, 1, 16, 4, 1)
+    YH_RW(2, 64, 2, 2, 1, 8, 3, 1)
+    YH_RW(2, 64, 2, 4, 1, 16, 2, 1)
+    YH_RW(2, 64, 4, 2, 1, 8, 3, 1)
+    YH_RW(2, 64, 4, 1, 1, 8, 4, 1)
+    // K-split (mx_kchunks): 128 / 256 input channels, one 64-channel chunk per wave
+    YH_RW(1, 128, 2, 2, 1, 8, 3, 2)
+    YH_RW(1, 128, 2, 1, 1, 8, 3, 2)
+    YH_RW(1, 128, 2, 1, 1, 8, 4, 2)
+    YH_RW(1, 128, 4, 1, 1, 8, 3, 2)
+    YH_RW(1, 256, 2, 1, 1, 8, 3, 4)
+    YH_RW(1, 256, 2, 1, 1, 4, 3, 4)
+    YH_RW(2, 128, 2, 2, 1, 8, 2, 2)
+    YH_RW(2, 128, 2, 1, 1, 8, 3, 2)
+    YH_RW(2, 128, 4, 1, 1, 8, 3, 2)
 #undef YH_RW
     return (int)hipErrorInvalidValue;
 }

@@ -946,7 +946,8 @@ struct Net {
     static std::string mx_name(const MxPlan& p) {
         char b[96];
         if (p.cfg.kind == 2)
-            snprintf(b, sizeof(b), "rw_g%d_p%d_mb%d_ns%d_t%dx%d", p.cfg.na, p.cfg.wm, p.cfg.mb, p.cfg.nbuf, p.TH, p.TW);
+            snprintf(b, sizeof(b), "rw_g%d_p%d_mb%d_ns%d_t%dx%d%s", p.cfg.na, p.cfg.wm, p.cfg.mb, p.cfg.nbuf, p.TH, p.TW,
+                     p.cfg.gdiv == 2 ? "_d2" : p.cfg.gdiv == 4 ? "_d4" : "");
         else
             snprintf(b, sizeof(b), "%s_na%d_mb%d_w%dx%d_ncb%d_t%dx%d", p.cfg.kind ? "mxr" : "mx", p.cfg.na, p.cfg.mb,
                      p.cfg.wn, p.cfg.wm, p.cfg.ncb, p.TH, p.TW);
