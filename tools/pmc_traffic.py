@@ -23,7 +23,7 @@ import re
 import sys
 
 FAMILY = {"stem": r"conv_first|stem_fused", "dwconv": r"dwconv", "sppf": r"sppf|maxpool",
-          "attention": r"psa_attention|pe_add", "decode": r"head_decode", "head_cls": r"head_cls", "box_dfl": r"box_dfl", "c3k2": r"csp_fused"}
+          "attention": r"psa_attention|pe_add", "decode": r"head_decode", "head_cls": r"head_cls", "box_dfl": r"box_dfl", "c3k2": r"csp_fused", "c3k": r"c3k_fused"}
 
 
 def dispatches(d, counter):

@@ -163,6 +163,20 @@ constexpr int HEAD_CLS_LDS = YH_HEAD_CLS_LDS_KB * 1024;   // 80: two workgroups 
 int head_cls_lds(int TH, int TW, int C0, int c3, int nc);
 int launch_head_cls(int dtype, const HeadClsArgs& a, hipStream_t s);
 
+// Fused C3k block (c3k.hip; nets/nn.py:52-63 CSPModule(c, c), c = 128, two Residual(64,
+// e=1.0)): one workgroup per image, every intermediate in LDS. Images of at most 512
+// pixels (v11_n's 20x20 stage at 640 x 640); bit-identical to the seven per-layer launches.
+struct C3kArgs {
+    const void* x; int ldx;          // block input (NHWC view, c channels)
+    void* y; int ldy;                // block output view (c channels)
+    int B, H, W;
+    const void* prm;                 // packed parameters (c3k_offsets)
+};
+int c3k_prm_bytes();
+void c3k_offsets(int (&off)[9]);     // w1, w2, residual convs, w3, b1, b2, residual biases, b3, total
+int c3k_lds(int H, int W);           // 0: the image does not fit
+int launch_c3k(int dtype, const C3kArgs& a, hipStream_t s);
+
 // Box tail of the detect head, one launch for all levels: the last box conv (Conv2d 1x1
 // + bias, nets/nn.py:241) with DFL (nn.py:222-225), make_anchors (utils/util.py:85-96) and
 // dist2bbox (nn.py:264-268) in its epilogue, writing rows 0..3 of y = io[1]. Bit-identical

@@ -75,7 +75,7 @@ static uint16_t f2h(float f) {
 
 // ---------------------------------------------------------------- graph model
 enum ConvKind { CK_DENSE = 0, CK_FIRST = 1, CK_DW = 2, CK_PE = 3 };
-enum OpKind { OP_FIRST, OP_CONV, OP_DW, OP_SPPF, OP_ATTN, OP_DECODE, OP_HEADCLS, OP_BOXDFL, OP_CSP, OP_STEM2 };
+enum OpKind { OP_FIRST, OP_CONV, OP_DW, OP_SPPF, OP_ATTN, OP_DECODE, OP_HEADCLS, OP_BOXDFL, OP_CSP, OP_STEM2, OP_C3K };
 static const char* op_kind_name(OpKind k) {
     switch (k) {
         case OP_FIRST: return "stem";
@@ -87,12 +87,13 @@ static const char* op_kind_name(OpKind k) {
         case OP_HEADCLS: return "head_cls";
         case OP_BOXDFL: return "box_dfl";
         case OP_CSP: return "c3k2";
+        case OP_C3K: return "c3k";
         case OP_STEM2: return "stem_fused";
     }
     return "unknown";
 }
 enum OpClass { CL_CONV3 = 0, CL_CONV1 = 1, CL_FIRST = 2, CL_DW = 3, CL_SPPF = 4, CL_ATTN = 5, CL_DECODE = 6,
-               CL_HEADCLS = 7, CL_BOXDFL = 8, CL_CSP = 9, CL_N = 10 };
+               CL_HEADCLS = 7, CL_BOXDFL = 8, CL_CSP = 9, CL_C3K = 10, CL_N = 11 };
 
 struct Tensor { int level; int C; };        // physical channels = pixel stride
 struct View { int t = -1; int coff = 0; int C = 0; };
@@ -137,6 +138,10 @@ struct Op {
     // OP_CSP: conv1, res_m.0.conv1, res_m.0.conv2, conv2 of a fused C3k2 block (in[0] -> out)
     // OP_STEM2: cs[0] = net.p2.0 (conv = the stem)
     int cs[4] = {-1, -1, -1, -1};
+    // OP_C3K: conv1, conv2, res_m.0.conv1, res_m.0.conv2, res_m.1.conv1, res_m.1.conv2, conv3 of
+    // a CSPModule, and the per-layer ops [alt0, alt1) it replaces at shapes where it fits
+    int ck[7] = {-1, -1, -1, -1, -1, -1, -1};
+    int alt0 = -1, alt1 = -1;
     std::string label;
 };
 
@@ -159,14 +164,16 @@ struct GraphKey {
 // (INTEGRATION.md lists them): YH_FUSE=0 turns every cross-layer fusion off (the
 // bit-identity tests compare both), YH_CSP_TAIL=1 forces the C3k2 tail mode where
 // the whole block would fit one launch (tested the same way), YH_CONV=<k> forces
-// candidate plan k of every 16-bit dense conv, YH_TUNE_LOG=1 prints the tuner's timings.
+// candidate plan k of every 16-bit dense conv, YH_TUNE_LOG=1 prints the tuner's timings,
+// YH_C3K=0 keeps the C3k blocks as per-layer launches (compared bit for bit by the tests).
 struct Options {
-    bool fuse = true, csp_tail = false, tune_log = false;
+    bool fuse = true, csp_tail = false, tune_log = false, c3k = true;
     int conv_force = -1;
     static Options from_env() {
         Options o;
         if (const char* e = getenv("YH_FUSE")) o.fuse = atoi(e) != 0;
         if (const char* e = getenv("YH_CSP_TAIL")) o.csp_tail = atoi(e) != 0;
+        if (const char* e = getenv("YH_C3K")) o.c3k = atoi(e) != 0;
         if (const char* e = getenv("YH_CONV")) o.conv_force = atoi(e);
         o.tune_log = getenv("YH_TUNE_LOG") != nullptr;
         return o;
@@ -205,7 +212,10 @@ struct Net {
     int num_cus = 0;
     // launch units of the forward at the current shape (one op each)
     struct Unit { int first, last; bool level; };
-    struct Plan { std::vector<Unit> units; };
+    struct Plan {
+        std::vector<Unit> units;
+        std::vector<char> active;   // per op: launched at this shape (fused blocks pick per shape)
+    };
     std::map<GraphKey, Plan> plans;
     const Plan* cur_plan = nullptr;
 
@@ -283,11 +293,25 @@ struct Net {
         const int t = tensor(level, 2 * h);
         View a = slice(t, 0, h), b = slice(t, h, h);
         const int a0 = tensor(level, h), a1 = tensor(level, h);
+        const int first = (int)ops.size();
         conv1(p + ".conv1", x, in_ch, h, ACT_SILU, full(a0));
         conv1(p + ".conv2", x, in_ch, h, ACT_SILU, b);
         residual(p + ".res_m.0", full(a0), h, 1.0, full(a1), level);
         residual(p + ".res_m.1", full(a1), h, 1.0, a, level);
         conv1(p + ".conv3", full(t), 2 * h, out_ch, ACT_SILU, out);
+        // 16-bit handles: the whole block as one launch (c3k.hip) at shapes whose image fits
+        // a workgroup's LDS (ensure_plan picks it or the seven launches above per shape)
+        if (dtype != F32 && opt.fuse && opt.c3k && in_ch == 128 && out_ch == 128 && x.C == 128) {
+            Op op;
+            op.kind = OP_C3K;
+            op.label = p;
+            for (int k = 0; k < 7; ++k) op.ck[k] = ops[first + k].conv;
+            op.in = {Seg{x, 0}};
+            op.out = out;
+            op.alt0 = first;
+            op.alt1 = (int)ops.size();
+            ops.push_back(op);
+        }
     }
     // CSP / C3k2 (nn.py:66-80); input may be a 2-segment (optionally upsampled) concat
     void csp(const std::string& p, const std::vector<Seg>& in, const std::vector<int>& logical, int out_ch, int n,
@@ -643,6 +667,59 @@ struct Net {
         HIPCHECK(hipMemcpy(dev, img.data(), img.size(), hipMemcpyHostToDevice));
         d0.mx_w.emplace("csp", dev);
         for (int k = k0 + 1; k < 4; ++k) convs[op.cs[k]].mx_w.emplace("csp_dep", nullptr);
+        return dev;
+    }
+    // packed parameters of a fused C3k block (c3k.hip layout), cached with its first conv
+    const void* c3k_params(const Op& op) {
+        ConvDesc& d0 = convs[op.ck[0]];
+        auto it = d0.mx_w.find("c3k");
+        bool ok = it != d0.mx_w.end();
+        for (int k = 1; k < 7; ++k) ok = ok && convs[op.ck[k]].mx_w.count("c3k_dep");
+        if (ok) return it->second;
+        if (it != d0.mx_w.end()) {
+            (void)hipFree(it->second);
+            d0.mx_w.erase(it);
+        }
+        for (int k = 0; k < 7; ++k) require(convs[op.ck[k]].loaded, "weights of " + convs[op.ck[k]].name + " not loaded", YH_ESTATE);
+        int off[9];
+        c3k_offsets(off);
+        std::vector<uint8_t> img((size_t)off[8], 0);
+        // fragment (tile a, step k, lane, j); rows: lane half hh of tile a holds couts
+        // 32a + 16hh .. +15 (c3k2.hip's order), or with bits 2 and 3 of the row swapped (rho:
+        // conv2, whose accumulators become conv3's B fragments)
+        auto frags = [&](int o, const ConvDesc& d, int ntile, int nk, bool rho) {
+            const int kk2 = d.k * d.k;
+            uint16_t* dst = reinterpret_cast<uint16_t*>(img.data() + o);
+            for (int a = 0; a < ntile; ++a)
+                for (int k = 0; k < nk; ++k)
+                    for (int lane = 0; lane < 64; ++lane)
+                        for (int j = 0; j < 8; ++j) {
+                            const int R = lane & 31, hh = lane >> 5;
+                            const int co = rho ? 32 * a + ((R & 0x13) | ((R & 4) << 1) | ((R & 8) >> 1))
+                                               : 32 * a + 16 * ((R >> 2) & 1) + (R & 3) + 4 * (R >> 3);
+                            const int cb = k / kk2, tap = k - cb * kk2, ch = 16 * cb + 8 * hh + j;
+                            float v = 0.f;
+                            if (co < d.cout && ch < d.cin) v = d.wf[((size_t)co * d.cin + ch) * kk2 + tap];
+                            dst[((size_t)(a * nk + k) * 64 + lane) * 8 + j] = dtype == BF16 ? f2bf(v) : f2h(v);
+                        }
+        };
+        frags(off[0], convs[op.ck[0]], 2, 8, false);
+        frags(off[1], convs[op.ck[1]], 2, 8, true);
+        for (int r = 0; r < 4; ++r) frags(off[2] + r * 2 * 36 * 1024, convs[op.ck[2 + r]], 2, 36, false);
+        frags(off[3], convs[op.ck[6]], 4, 8, false);
+        auto biases = [&](int o, const ConvDesc& d) {
+            float* dst = reinterpret_cast<float*>(img.data() + o);
+            for (int i = 0; i < d.cout; ++i) dst[i] = d.bf[i];
+        };
+        biases(off[4], convs[op.ck[0]]);
+        biases(off[5], convs[op.ck[1]]);
+        for (int r = 0; r < 4; ++r) biases(off[6] + r * 64 * 4, convs[op.ck[2 + r]]);
+        biases(off[7], convs[op.ck[6]]);
+        void* dev = nullptr;
+        HIPCHECK(hipMalloc(&dev, img.size()));
+        HIPCHECK(hipMemcpy(dev, img.data(), img.size(), hipMemcpyHostToDevice));
+        d0.mx_w.emplace("c3k", dev);
+        for (int k = 1; k < 7; ++k) convs[op.ck[k]].mx_w.emplace("c3k_dep", nullptr);
         return dev;
     }
     // the decode folds into box_dfl + head_cls / a class-rows decode (16-bit handles; the
@@ -1034,19 +1111,22 @@ struct Net {
         hipEvent_t e0, e1;
         HIPCHECK(hipEventCreate(&e0));
         HIPCHECK(hipEventCreate(&e1));
+        const std::vector<char>& act = cur_plan->active;
         for (size_t i = 0; i < ops.size(); ++i) {
-            if (ops[i].kind != OP_CONV || cands[i].size() < 2) continue;
+            if (ops[i].kind != OP_CONV || cands[i].size() < 2 || !act[i]) continue;
+            int prev = (int)i - 1;
+            while (prev >= 0 && !act[prev]) --prev;
             std::vector<float> t_ms(cands[i].size(), 0.f);
             for (size_t c = 0; c < cands[i].size(); ++c) {
                 const MxPlan& pl = cands[i][c];
                 int rc = launch_mx_op(ops[i], pl, B, H, W, s);
                 float ms = 0.f;
-                if (i > 0) {
+                if (prev >= 0) {
                     // in situ: each timed launch right after the op that precedes it in the
                     // forward, so the input's cache state (just written, L2 / MALL warm, the
                     // layer's other operands cold) is the forward's, not a back-to-back loop's
                     for (int r = 0; r < 3 && rc == 0; ++r) {
-                        launch_op(i - 1, B, H, W, s);
+                        launch_op((size_t)prev, B, H, W, s);
                         HIPCHECK(hipEventRecord(e0, s));
                         rc = launch_mx_op(ops[i], pl, B, H, W, s);
                         HIPCHECK(hipEventRecord(e1, s));
@@ -1270,6 +1350,21 @@ struct Net {
                 rc = launch_csp(dtype, a, std::min(a.ntiles, 2 * num_cus), s);
                 break;
             }
+            case OP_C3K: {
+                C3kArgs a{};
+                const View& xv = op.in[0].v;
+                const int lv = tensors[xv.t].level;
+                a.x = ptr(xv);
+                a.ldx = ldc(xv);
+                a.y = ptr(op.out);
+                a.ldy = ldc(op.out);
+                a.H = H >> lv;
+                a.W = W >> lv;
+                a.B = B;
+                a.prm = c3k_params(op);
+                rc = launch_c3k(dtype, a, s);
+                break;
+            }
         }
         if (rc != 0) throw Fail(YH_EHIP, "launch of " + op.label + " failed: " + hipGetErrorString((hipError_t)rc));
     }
@@ -1285,7 +1380,19 @@ struct Net {
         auto it = plans.find(key);
         if (it != plans.end()) { cur_plan = &it->second; return; }
         Plan pl;
-        for (size_t i = 0; i < ops.size(); ++i) pl.units.push_back(Unit{(int)i, (int)i + 1, false});
+        // a fused C3k block runs where one image fits a workgroup's LDS (c3k_lds), its seven
+        // per-layer launches everywhere else
+        pl.active.assign(ops.size(), 1);
+        for (size_t i = 0; i < ops.size(); ++i) {
+            if (ops[i].kind != OP_C3K) continue;
+            const int lv = tensors[ops[i].out.t].level;
+            if (c3k_lds(H >> lv, W >> lv) > 0)
+                for (int k = ops[i].alt0; k < ops[i].alt1; ++k) pl.active[k] = 0;
+            else
+                pl.active[i] = 0;
+        }
+        for (size_t i = 0; i < ops.size(); ++i)
+            if (pl.active[i]) pl.units.push_back(Unit{(int)i, (int)i + 1, false});
         cur_plan = &plans.emplace(key, std::move(pl)).first->second;
     }
     void launch_unit(const Unit& u, int B, int H, int W, hipStream_t s) {
@@ -1378,6 +1485,7 @@ struct Net {
             case OP_BOXDFL: return CL_BOXDFL;
             case OP_CSP: return CL_CSP;
             case OP_STEM2: return CL_FIRST;
+            case OP_C3K: return CL_C3K;
         }
         return CL_CONV1;
     }
@@ -1475,6 +1583,19 @@ struct Net {
                     if (op.cs[k] < 0) continue;   // tail mode: conv1 is its own op
                     const ConvDesc* d = &convs[op.cs[k]];
                     const double macs = (double)d->cout * d->cin * d->k * d->k;
+                    bytes += macs * es;
+                    flops += 2.0 * n * macs;
+                }
+                break;
+            }
+            case OP_C3K: {
+                // block input read once (conv1 and conv2 share it), block output written once,
+                // the seven convs' weights once
+                const double n = px(tensors[op.out.t].level);
+                bytes = n * op.in[0].v.C * es + n * convs[op.ck[6]].cout * es;
+                for (int k = 0; k < 7; ++k) {
+                    const ConvDesc& d = convs[op.ck[k]];
+                    const double macs = (double)d.cout * d.cin * d.k * d.k;
                     bytes += macs * es;
                     flops += 2.0 * n * macs;
                 }

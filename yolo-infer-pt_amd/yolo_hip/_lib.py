@@ -16,7 +16,7 @@ if os.environ.get("YH_LIB"):
     LIB_PATH = os.environ["YH_LIB"]
 
 YH_F32, YH_F16, YH_BF16 = 0, 1, 2
-ABI_VERSION = 2
+ABI_VERSION = 3
 
 
 class YhVariant(ctypes.Structure):
