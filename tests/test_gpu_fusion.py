@@ -96,3 +96,25 @@ def test_fused_stem_uint8_input(gpu, variant, dtype, batch, h, w):
     yp = plain.forward(x8).clone()
     assert torch.equal(yf, yp), (yf.float() - yp.float()).abs().max().item()
     assert torch.equal(fused.forward(x8.to(dtype) / 255), yf)
+
+
+@pytest.mark.parametrize("dtype,batch,h,w,fits", [(torch.bfloat16, 2, 640, 640, True), (torch.float16, 3, 96, 160, True),
+                                                  (torch.bfloat16, 1, 1280, 1280, False)])
+def test_c3k_block_equals_per_layer_launches(gpu, dtype, batch, h, w, fits):
+    """c3k.hip: a CSPModule(128, 128) block (v11_n net.p5.1 / fpn.h6) in one launch per image
+    where the 20x20-stage image fits the LDS, the seven per-layer launches elsewhere (40x40 at
+    1280); YH_C3K=0 keeps the per-layer launches everywhere. Bit-identical either way."""
+    model = make_model("n")
+    x = synth.synth_scenes(batch, h, w, seed=37).to(gpu, dtype)
+    fused = _engine(model, dtype, gpu, True)
+    plain = _engine(model, dtype, gpu, True, YH_C3K="0")
+    yf = fused.forward(x).clone()
+    yp = plain.forward(x).clone()
+    kinds_f = [u["cls"] for u in fused.units(batch, h, w)]
+    kinds_p = [u["cls"] for u in plain.units(batch, h, w)]
+    assert "c3k" not in kinds_p
+    assert (kinds_f.count("c3k") == 2) == fits, kinds_f
+    if fits:   # seven launches -> one, twice
+        assert len(kinds_p) - len(kinds_f) == 12
+    assert torch.isfinite(yf.float()).all()
+    assert torch.equal(yf, yp), (yf.float() - yp.float()).abs().max().item()
