@@ -8,7 +8,7 @@
 //   C   C1 = r0.conv2(T) + C1    3x3 h -> h, + SiLU, + residual       in place (nn.py:49)
 //   D   T  = r1.conv1(C1)
 //   E   C1 = r1.conv2(T) + C1
-//   F   y  = conv3([C1 | conv2(x)])  1x1 2h -> c, + SiLU             conv2 recomputed per tile
+//   F   y  = conv3([C1 | c2])    1x1 2h -> c, + SiLU             c2 = conv2(x), from phase A
 // Each 3x3 conv runs as two sub-phases, one per 32-cout tile; the tile's 36-step weight
 // image comes by LDS-DMA in two 18 KB halves that ping-pong between two buffers, the next
 // half in flight while the current one is multiplied (one copy per workgroup, read by every
@@ -21,6 +21,8 @@
 // (pack2, as mx_epi); the residual is added to the rounded value in fp32 and rounded again.
 #include "common.h"
 #include "dtypes.h"
+
+#include <algorithm>
 
 namespace yh {
 
@@ -107,21 +109,32 @@ namespace {
 template <typename T>
 __global__ __launch_bounds__(CK_THREADS, 1) void c3k_fused(const C3kArgs A) {
     constexpr CkLayout L = ck_layout();
+    constexpr int WBH = 18 * 1024;                   // one weight half (18 of a tile's 36 steps)
     extern __shared__ __attribute__((aligned(1024))) char sm[];
     typedef __attribute__((address_space(3))) char* lds_c;
     const unsigned lds0 = (unsigned)(size_t)(lds_c)sm;
     const int HW = A.H * A.W;
     char* C1 = sm;                                   // [HW][64] (swizzled chunks)
-    char* TT = sm + HW * CK_PX;                      // [HW][64]
-    const int wb_off = 2 * HW * CK_PX;               // one 3x3 tile's weights: 36 KB
+    char* TT = sm + HW * CK_PX;                      // [HW][64]; conv3's 32 KB of weights in phase F
+    const int wb_off = HW * CK_PX + (HW * CK_PX > 32 * 1024 ? HW * CK_PX : 32 * 1024);   // two weight halves
     char* WB = sm + wb_off;
-    char* ZR = WB + 36 * 1024;                       // 128 zero bytes (out-of-image taps)
+    char* ZR = WB + 2 * WBH;                         // 128 zero bytes (out-of-image taps)
+    const float* BI = reinterpret_cast<const float*>(ZR + 128);   // every bias (2 KB)
     const int lane = threadIdx.x & 63, l32 = lane & 31, h = lane >> 5;
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int n = blockIdx.x;
     const char* prm = reinterpret_cast<const char*>(A.prm);
-    const float* bias = reinterpret_cast<const float*>(prm + L.b1);
+    // LDS-DMA of `kb` 1-KB pieces from the parameter image at `src` to LDS offset `dst`
+    auto dma = [&](int src, int dst, int kb) {
+        for (int i = wv; i < kb; i += CK_NW) ck_glds(prm + src + i * 1024 + lane * 16, lds0 + (unsigned)(dst + i * 1024));
+    };
 
+    // prologue: conv1's weights into the second weight buffer, conv2's into T (free until the
+    // first Residual conv writes it), the biases, the first 3x3 half
+    dma(L.w1, wb_off + WBH, 16);
+    dma(L.w2, (int)(TT - sm), 16);
+    dma(L.b1, (int)((const char*)BI - sm), (L.total - L.b1) / 1024);
+    dma(L.wr, wb_off, 18);
     if (threadIdx.x < 8) *reinterpret_cast<uint4*>(ZR + threadIdx.x * 16) = make_uint4(0, 0, 0, 0);
     // the wave's pixel tile: 32 consecutive pixels (clamped; only p < HW is written)
     const int p = wv * 32 + l32;
@@ -130,22 +143,48 @@ __global__ __launch_bounds__(CK_THREADS, 1) void c3k_fused(const C3kArgs A) {
     const int pc = pv ? p : HW - 1;
     const int py = pc / A.W, px = pc - py * A.W;
     const T* xp = reinterpret_cast<const T*>(A.x) + ((long long)n * HW + pc) * A.ldx + 8 * h;
-
-    // ---- A: C1 = SiLU(conv1(x)); B fragments straight from HBM, A fragments from L2
-    if (own) {
-        uint4 xb[8];
+    uint4 xb[8];
 #pragma unroll
-        for (int kb = 0; kb < 8; ++kb) xb[kb] = *reinterpret_cast<const uint4*>(xp + 16 * kb);
-        const uint4* w1 = reinterpret_cast<const uint4*>(prm + L.w1) + lane;
+    for (int kb = 0; kb < 8; ++kb) xb[kb] = *reinterpret_cast<const uint4*>(xp + 16 * kb);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    ck_barrier();
+
+    // ---- A: C1 = SiLU(conv1(x)) -> LDS; conv2(x) -> registers (its rows permuted: registers
+    //      8 jj .. + 7 of tile t are channels 32 t + 16 jj + 8 h .. + 7 = conv3's B fragment of
+    //      K block 4 + 2 t + jj), held until phase F. B fragments from HBM, A from LDS.
+    uint4 bf[8];
+    f32x16 acc;
+    if (own) {
+        const char* w2 = TT;
+        const float* b2 = BI + (L.b2 - L.b1) / 4;
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+#pragma unroll
+            for (int e = 0; e < 16; ++e) acc[e] = 0.f;
+#pragma unroll
+            for (int kb = 0; kb < 8; ++kb)
+                acc = KMfma<T>::step(*reinterpret_cast<const uint4*>(w2 + ((t * 8 + kb) * 64 + lane) * 16), xb[kb], acc);
+#pragma unroll
+            for (int jj = 0; jj < 2; ++jj) {
+                const float* bj = b2 + 32 * t + 16 * jj + 8 * h;
+                unsigned w[4];
+#pragma unroll
+                for (int e = 0; e < 8; e += 2)
+                    w[e >> 1] = ck_pack2<T>(silu<T>(acc[8 * jj + e] + bj[e]), silu<T>(acc[8 * jj + e + 1] + bj[e + 1]));
+                bf[4 + 2 * t + jj] = make_uint4(w[0], w[1], w[2], w[3]);
+            }
+        }
+        const char* w1 = WB + WBH;
 #pragma unroll
         for (int t = 0; t < 2; ++t) {
             f32x16 acc;
 #pragma unroll
             for (int e = 0; e < 16; ++e) acc[e] = 0.f;
 #pragma unroll
-            for (int kb = 0; kb < 8; ++kb) acc = KMfma<T>::step(w1[(t * 8 + kb) * 64], xb[kb], acc);
+            for (int kb = 0; kb < 8; ++kb)
+                acc = KMfma<T>::step(*reinterpret_cast<const uint4*>(w1 + ((t * 8 + kb) * 64 + lane) * 16), xb[kb], acc);
             unsigned w[8];
-            ck_act<T>(acc, bias + 32 * t + 16 * h, w);
+            ck_act<T>(acc, BI + 32 * t + 16 * h, w);
             if (pv) {
                 *reinterpret_cast<uint4*>(C1 + ck_off(p, 4 * t + 2 * h)) = make_uint4(w[0], w[1], w[2], w[3]);
                 *reinterpret_cast<uint4*>(C1 + ck_off(p, 4 * t + 2 * h + 1)) = make_uint4(w[4], w[5], w[6], w[7]);
@@ -153,29 +192,22 @@ __global__ __launch_bounds__(CK_THREADS, 1) void c3k_fused(const C3kArgs A) {
         }
     }
 
-    // 3x3 taps of the wave's pixel: pixel byte offset within C1 / T (-1: outside the image,
-    // read from the zero block) and chunk swizzle
-    int tq[9], ts[9];
+    // 3x3 taps of the wave's pixel: pixel byte offset within C1 / T with the chunk swizzle in
+    // its low bits (-128: outside the image, read from the zero block)
+    int tq[9];
 #pragma unroll
     for (int t = 0; t < 9; ++t) {
         const int yy = py + t / 3 - 1, xx = px + t % 3 - 1;
         const bool in = (unsigned)yy < (unsigned)A.H && (unsigned)xx < (unsigned)A.W;
         const int q = yy * A.W + xx;
-        tq[t] = in ? q * CK_PX : -1;
-        ts[t] = in ? ((q >> 1) & 7) : 0;
+        tq[t] = in ? (q * CK_PX) | ((q >> 1) & 7) : -CK_PX;
     }
     const int zr_off = (int)(ZR - sm);
 
     // ---- B..E: the Residual convs, one 32-cout tile per sub-phase. A tile's 36 weight steps
     //      arrive as two 18 KB halves that ping-pong between two LDS buffers: the next half
-    //      (of this tile or the next one) is DMA'd while the current half is multiplied.
-    auto issue_w = [&](int hs) {   // half-step hs = (conv * 2 + tile) * 2 + half -> buffer hs & 1
-        const char* wsrc = prm + L.wr + hs * 18 * 1024;
-        for (int i = wv; i < 18; i += CK_NW)
-            ck_glds(wsrc + i * 1024 + lane * 16, lds0 + (unsigned)(wb_off + (hs & 1) * 18 * 1024 + i * 1024));
-    };
-    issue_w(0);
-    f32x16 acc;
+    //      (of this tile or the next one; after the last one, conv3's first two tiles) is
+    //      DMA'd while the current half is multiplied.
 #pragma unroll 1
     for (int hs = 0; hs < 16; ++hs) {
         const int cv = hs >> 2, t = (hs >> 1) & 1, half = hs & 1;
@@ -183,29 +215,30 @@ __global__ __launch_bounds__(CK_THREADS, 1) void c3k_fused(const C3kArgs A) {
         char* dst = (cv & 1) ? C1 : TT;
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's DMAs of half-step hs
         ck_barrier();   // ... and everyone's; the other buffer and the previous phase are done
-        if (hs + 1 < 16) issue_w(hs + 1);
+        if (hs + 1 < 16) dma(L.wr + (hs + 1) * WBH, wb_off + ((hs + 1) & 1) * WBH, 18);
+        else dma(L.w3, wb_off, 16);
         if (!own) continue;
         const int src_off = (int)(src - sm);
         int tb[9];
 #pragma unroll
-        for (int k = 0; k < 9; ++k) tb[k] = tq[k] >= 0 ? src_off + tq[k] : zr_off;
+        for (int k = 0; k < 9; ++k) tb[k] = tq[k] >= 0 ? src_off + (tq[k] & ~(CK_PX - 1)) : zr_off;
         if (half == 0) {
 #pragma unroll
             for (int e = 0; e < 16; ++e) acc[e] = 0.f;
         }
-        const char* wb = WB + half * 18 * 1024;
+        const char* wb = WB + half * WBH;
 #pragma unroll 1
         for (int cb = 2 * half; cb < 2 * half + 2; ++cb)
 #pragma unroll
             for (int k = 0; k < 9; ++k) {
                 const uint4 a = *reinterpret_cast<const uint4*>(wb + (((cb & 1) * 9 + k) * 64 + lane) * 16);
-                const uint4 b = *reinterpret_cast<const uint4*>(sm + tb[k] + (((2 * cb + h) ^ ts[k]) << 4));
+                const uint4 b = *reinterpret_cast<const uint4*>(sm + tb[k] + (((2 * cb + h) ^ (tq[k] & 7)) << 4));
                 acc = KMfma<T>::step(a, b, acc);
+                if (k % 3 == 2) asm volatile("" ::: "memory");   // 3 taps' reads in flight (VGPR budget)
             }
         if (half == 0) continue;
-        const float* bb = bias + (L.br - L.b1) / 4 + 64 * cv;
         unsigned w[8];
-        ck_act<T>(acc, bb + 32 * t + 16 * h, w);
+        ck_act<T>(acc, BI + (L.br - L.b1) / 4 + 64 * cv + 32 * t + 16 * h, w);
         if (pv) {
             const int o0 = ck_off(p, 4 * t + 2 * h), o1 = ck_off(p, 4 * t + 2 * h + 1);
             if (cv & 1) {   // conv2 of a Residual: + its input (C1), rounded again (nn.py:49)
@@ -219,49 +252,30 @@ __global__ __launch_bounds__(CK_THREADS, 1) void c3k_fused(const C3kArgs A) {
             *reinterpret_cast<uint4*>(dst + o1) = make_uint4(w[4], w[5], w[6], w[7]);
         }
     }
+    // ---- F: conv3 over [C1 | conv2] -> y; its tiles 0-1 from the first buffer (landed during
+    //      the last half-step), tiles 2-3 from the second (DMA'd now, while 0-1 multiply)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     ck_barrier();
-
-    // ---- F: conv2(x) into registers (its rows permuted: registers 8 jj .. + 7 of tile t are
-    //      channels 32 t + 16 jj + 8 h .. + 7 = conv3's B fragment of K block 4 + 2 t + jj),
-    //      then conv3 over [C1 | conv2] -> y
-    if (!own) return;
-    uint4 bf[8];
-    {
-        uint4 xb[8];
+    dma(L.w3 + 16 * 1024, wb_off + WBH, 16);
+    const float* b3 = BI + (L.b3 - L.b1) / 4;
+    T* y = reinterpret_cast<T*>(A.y) + ((long long)n * HW + pc) * A.ldy;
+    if (own) {
 #pragma unroll
-        for (int kb = 0; kb < 8; ++kb) xb[kb] = *reinterpret_cast<const uint4*>(xp + 16 * kb);
-        const uint4* w2 = reinterpret_cast<const uint4*>(prm + L.w2) + lane;
-        const float* b2 = bias + (L.b2 - L.b1) / 4;
-#pragma unroll
-        for (int t = 0; t < 2; ++t) {
-            f32x16 acc;
-#pragma unroll
-            for (int e = 0; e < 16; ++e) acc[e] = 0.f;
-#pragma unroll
-            for (int kb = 0; kb < 8; ++kb) acc = KMfma<T>::step(w2[(t * 8 + kb) * 64], xb[kb], acc);
-#pragma unroll
-            for (int jj = 0; jj < 2; ++jj) {
-                const float* bj = b2 + 32 * t + 16 * jj + 8 * h;
-                unsigned w[4];
-#pragma unroll
-                for (int e = 0; e < 8; e += 2)
-                    w[e >> 1] = ck_pack2<T>(silu<T>(acc[8 * jj + e] + bj[e]), silu<T>(acc[8 * jj + e + 1] + bj[e + 1]));
-                bf[4 + 2 * t + jj] = make_uint4(w[0], w[1], w[2], w[3]);
-            }
-        }
+        for (int kb = 0; kb < 4; ++kb) bf[kb] = *reinterpret_cast<const uint4*>(C1 + ck_off(pc, 2 * kb + h));
     }
 #pragma unroll
-    for (int kb = 0; kb < 4; ++kb) bf[kb] = *reinterpret_cast<const uint4*>(C1 + ck_off(pc, 2 * kb + h));
-    const uint4* w3 = reinterpret_cast<const uint4*>(prm + L.w3) + lane;
-    const float* b3 = bias + (L.b3 - L.b1) / 4;
-    T* y = reinterpret_cast<T*>(A.y) + ((long long)n * HW + pc) * A.ldy;
-#pragma unroll
     for (int t = 0; t < 4; ++t) {
-        f32x16 acc;
+        if (t == 2) {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            ck_barrier();
+        }
+        if (!own) continue;
+        const char* w3 = WB + (t >> 1) * WBH + (t & 1) * 8 * 1024;
 #pragma unroll
         for (int e = 0; e < 16; ++e) acc[e] = 0.f;
 #pragma unroll
-        for (int kb = 0; kb < 8; ++kb) acc = KMfma<T>::step(w3[(t * 8 + kb) * 64], bf[kb], acc);
+        for (int kb = 0; kb < 8; ++kb)
+            acc = KMfma<T>::step(*reinterpret_cast<const uint4*>(w3 + (kb * 64 + lane) * 16), bf[kb], acc);
         unsigned w[8];
         ck_act<T>(acc, b3 + 32 * t + 16 * h, w);
         if (pv) {
@@ -299,7 +313,9 @@ void c3k_offsets(int (&off)[9]) {
 int c3k_lds(int H, int W) {
     const long long hw = (long long)H * W;
     if (H < 1 || W < 1 || hw > 32 * CK_NW) return 0;
-    const long long b = 2 * hw * CK_PX + 36 * 1024 + 128;
+    // C1 + T (T also holds conv3's 32 KB of weights in the last phase), two 18 KB weight
+    // halves, the zero block, the biases
+    const long long b = hw * CK_PX + std::max(hw * CK_PX, 32LL * 1024) + 36 * 1024 + 128 + (ck_layout().total - ck_layout().b1);
     return b <= 160 * 1024 ? (int)b : 0;
 }
 
