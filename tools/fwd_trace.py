@@ -53,7 +53,7 @@ def main():
     os.makedirs(os.path.dirname(out), exist_ok=True)
     with open(out, "w") as f:
         json.dump(dict(forwards=nf, ops=[dict(label=o["label"], cls=o["cls"], bytes=o["bytes"], flops=o["flops"],
-                                              kernel=o["kernel"]) for o in eng.ops(B, size, size)]), f)
+                                              kernel=o["kernel"]) for o in (u["ops"][0] for u in eng.units(B, size, size))]), f)
     print("fwd_trace done", flush=True)
 
 

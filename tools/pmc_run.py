@@ -49,7 +49,7 @@ def main():
         with open(out, "w") as f:
             json.dump(dict(config=dict(variant=v, size=size, batch=B, dtype="bf16"),
                            ops=[dict(label=o["label"], cls=o["cls"], bytes=o["bytes"], kernel=o["kernel"])
-                                for o in eng.ops(B, size, size)]), f)
+                                for o in (u["ops"][0] for u in eng.units(B, size, size))]), f)
     print("pmc workload done", flush=True)
 
 

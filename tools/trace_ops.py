@@ -13,12 +13,16 @@ import re
 import statistics
 import sys
 
-FAMILY = {  # dispatch-name patterns per op class; convs take exactly one dispatch
-    "first": r"conv_first|stem_fused",
-    "dw": r"dwconv",
+FAMILY = {  # dispatch-name patterns per op class (yolo_hip.engine.OP_CLASSES); convs take exactly one dispatch
+    "stem": r"conv_first|stem_fused",
+    "dwconv": r"dwconv",
     "sppf": r"sppf|maxpool",
-    "attn": r"psa_attention|pe_add",
+    "attention": r"psa_attention|pe_add",
     "decode": r"head_decode",
+    "head_cls": r"head_cls",
+    "box_dfl": r"box_dfl",
+    "c3k2": r"csp_fused",
+    "c3k": r"c3k_fused",
 }
 
 
