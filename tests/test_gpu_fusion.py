@@ -118,3 +118,25 @@ def test_c3k_block_equals_per_layer_launches(gpu, dtype, batch, h, w, fits):
         assert len(kinds_p) - len(kinds_f) == 12
     assert torch.isfinite(yf.float()).all()
     assert torch.equal(yf, yp), (yf.float() - yp.float()).abs().max().item()
+
+
+@pytest.mark.parametrize("dtype,batch,h,w", [(torch.bfloat16, 2, 640, 640), (torch.float16, 3, 96, 160),
+                                             (torch.bfloat16, 1, 352, 480)])
+def test_head_cls_wide_level_equals_per_layer_launches(gpu, dtype, batch, h, w):
+    """head.hip: v11_n's 20x20 cls branch (256 input channels: four 64-channel dw1 chunks, pw1
+    over 16 K blocks in two halves) joins the fused head_cls launch, and with every level fused
+    the class-rows decode disappears (5 + 1 launches fewer); YH_HCLS_WIDE=0 keeps its per-layer
+    launches. Bit-identical either way."""
+    model = make_model("n")
+    x = synth.synth_scenes(batch, h, w, seed=41).to(gpu, dtype)
+    wide = _engine(model, dtype, gpu, True)
+    plain = _engine(model, dtype, gpu, True, YH_HCLS_WIDE="0")
+    yf = wide.forward(x).clone()
+    yp = plain.forward(x).clone()
+    lf = [u["label"] for u in wide.units(batch, h, w)]
+    lp = [u["label"] for u in plain.units(batch, h, w)]
+    assert "head.decode_cls" in lp and "head.cls.2.1" in lp, lp
+    assert not any(l.startswith("head.cls.") or l.startswith("head.decode") for l in lf), lf
+    assert len(lp) - len(lf) == 6
+    assert torch.isfinite(yf.float()).all()
+    assert torch.equal(yf, yp), (yf.float() - yp.float()).abs().max().item()

@@ -165,15 +165,17 @@ struct GraphKey {
 // bit-identity tests compare both), YH_CSP_TAIL=1 forces the C3k2 tail mode where
 // the whole block would fit one launch (tested the same way), YH_CONV=<k> forces
 // candidate plan k of every 16-bit dense conv, YH_TUNE_LOG=1 prints the tuner's timings,
-// YH_C3K=0 keeps the C3k blocks as per-layer launches (compared bit for bit by the tests).
+// YH_C3K=0 keeps the C3k blocks as per-layer launches (compared bit for bit by the tests),
+// YH_HCLS_WIDE=0 keeps a 256-channel level's cls branch (v11_n 20x20) as per-layer launches.
 struct Options {
-    bool fuse = true, csp_tail = false, tune_log = false, c3k = true;
+    bool fuse = true, csp_tail = false, tune_log = false, c3k = true, hcls_wide = true;
     int conv_force = -1;
     static Options from_env() {
         Options o;
         if (const char* e = getenv("YH_FUSE")) o.fuse = atoi(e) != 0;
         if (const char* e = getenv("YH_CSP_TAIL")) o.csp_tail = atoi(e) != 0;
         if (const char* e = getenv("YH_C3K")) o.c3k = atoi(e) != 0;
+        if (const char* e = getenv("YH_HCLS_WIDE")) o.hcls_wide = atoi(e) != 0;
         if (const char* e = getenv("YH_CONV")) o.conv_force = atoi(e);
         o.tune_log = getenv("YH_TUNE_LOG") != nullptr;
         return o;
@@ -739,6 +741,7 @@ struct Net {
     bool fuse_head_cls(int C0, int c3, int nc) const {
         if (dtype == F32 || !opt.fuse) return false;
         if (c3 % 16 || nc % 4 || C0 % 16) return false;
+        if (C0 > 128 && !opt.hcls_wide) return false;
         int TH, TW;
         return head_cls_tile(C0, c3, nc, 1 << 30, 1 << 30, TH, TW);
     }
@@ -1180,8 +1183,10 @@ struct Net {
         int l0 = 0;
         while (!op.hlv[l0]) ++l0;
         a.c3 = convs[op.hc[l0][1]].cout;
+        // workgroup order: the 20x20 level first (four input-channel chunks per tile, the
+        // longest workgroups), then 80x80 and 40x40
         int lvls[3], nl = 0;
-        for (int l = 0; l < 3; ++l)
+        for (int l : {2, 0, 1})
             if (op.hlv[l]) lvls[nl++] = l;
         for (int k = 0; k < nl; ++k) {
             const int l = lvls[k];
@@ -1212,7 +1217,7 @@ struct Net {
             a.io = (const void* const*)io_dev;
             a.A = anchor_off(3, H, W);
         }
-        // one workgroup per tile, the 80x80 level (most work) first
+        // one workgroup per tile, levels in lvls order
         int wg = 0;
         for (int k = 0; k < nl; ++k) {
             a.lv[k].wg0 = wg;

@@ -217,6 +217,63 @@ __device__ __forceinline__ void hc_pw_run(const T* src, int ss, int NPX, const T
     }
 }
 
+template <int NK>
+struct HcA<NK, 0> {};
+
+// Pointwise phase for wide K (NK > 8: the 256-channel 20x20 level's pw1): the work units are
+// (32-pixel B tile, 32-cout A tile) pairs round-robin over the waves, and K runs in 8-block
+// halves, the next half's A (global) and B (LDS) fragments loading while the current half's
+// MFMAs run. One fp32 chain per unit over the 16-channel blocks in ascending order: the same
+// K order, the same bits as hc_pw_run and the per-layer 1x1 conv.
+template <typename T, int NK, typename Store>
+__device__ __forceinline__ void hc_pw_wide(const T* src, int ss, int NPX, const T* w, int wld, const float* bias, int M,
+                                           bool silu_act, Store store) {
+    static_assert(NK % 8 == 0, "whole 8-block halves");
+    constexpr int NH = NK / 8;
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int l32 = lane & 31, h = lane >> 5;
+    const int na = (M + 31) >> 5, nb = (NPX + 31) >> 5;
+    hc_barrier();   // src complete
+    for (int u = wv; u < na * nb; u += NWV) {
+        const int bi = u / na, a = u - bi * na;
+        const int px = bi * 32 + l32;
+        const int pxc = px < NPX ? px : NPX - 1;
+        const T* brow = src + pxc * ss + 8 * h;
+        const T* wrow = w + (long long)(a * 32 + l32) * wld + 8 * h;
+        uint4 af[2][8], bf[2][8];
+        auto load = [&](int hh, int buf) {
+#pragma unroll
+            for (int kb = 0; kb < 8; ++kb) {
+                af[buf][kb] = *reinterpret_cast<const uint4*>(wrow + (hh * 8 + kb) * 16);
+                bf[buf][kb] = *reinterpret_cast<const uint4*>(brow + (hh * 8 + kb) * 16);
+            }
+        };
+        load(0, 0);
+        f32x16 acc;
+#pragma unroll
+        for (int e = 0; e < 16; ++e) acc[e] = 0.f;
+#pragma unroll
+        for (int hh = 0; hh < NH; ++hh) {
+            if (hh + 1 < NH) load(hh + 1, (hh + 1) & 1);
+#pragma unroll
+            for (int kb = 0; kb < 8; ++kb) acc = HMfma<T>::step(af[hh & 1][kb], bf[hh & 1][kb], acc);
+        }
+        if (px < NPX) {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int co = a * 32 + 8 * q + 4 * h;
+                if (co >= M) continue;
+                const float4 bb = *reinterpret_cast<const float4*>(bias + co);
+                float v[4] = {acc[4 * q] + bb.x, acc[4 * q + 1] + bb.y, acc[4 * q + 2] + bb.z, acc[4 * q + 3] + bb.w};
+                T o4[4];
+#pragma unroll
+                for (int e = 0; e < 4; ++e) o4[e] = fromf<T>(silu_act ? silu<T>(v[e]) : v[e]);
+                store(px, co, *reinterpret_cast<const uint2*>(o4));
+            }
+        }
+    }
+}
+
 // One workgroup = one output tile of level li. NK1 = C0 / 16 and NK2 = c3 / 16 (K blocks of
 // the first and the later pointwise convs); NAP1 = pw1 A tiles loaded ahead (all three when
 // the registers allow).
@@ -264,7 +321,7 @@ __device__ __forceinline__ void hc_body(const HeadClsArgs& A, int li, char* hsm)
     }
     const T* x = reinterpret_cast<const T*>(V.x);
     HcA<NK1, NAP1> A1;   // pw1's weights, in flight while the input tile loads
-    hc_pw_pre<T, NK1, NAP1>(reinterpret_cast<const T*>(V.pw1w), V.pw1ld, c3, A1);
+    if constexpr (NAP1 > 0) hc_pw_pre<T, NK1, NAP1>(reinterpret_cast<const T*>(V.pw1w), V.pw1ld, c3, A1);
 
     // 1-2. per 64-channel chunk: input tile with a 2-pixel halo (zeros outside the image =
     //      dw1's zero padding) -> R1, then dw1 of the chunk over the MH x MW mid region -> R2
@@ -290,14 +347,17 @@ __device__ __forceinline__ void hc_body(const HeadClsArgs& A, int li, char* hsm)
         if (cl + ck < C0) hc_barrier();   // the next chunk overwrites R1
     }
     // 3. pw1: D1 (R2) -> P1 (R1), zero outside the image (dw2's zero padding)
-    hc_pw_run<T, NK1, NAP1>(R2, L.SD, MH * MW, reinterpret_cast<const T*>(V.pw1w), V.pw1ld, QB1, c3, true, A1,
-                                [&](int px, int co, uint2 v) {
-                                    const int r = px / MW, cc = px - r * MW;
-                                    const int gh = h0 - 1 + r, gw = w0 - 1 + cc;
-                                    if (!((unsigned)gh < (unsigned)H && (unsigned)gw < (unsigned)W))
-                                        v = make_uint2(0, 0);
-                                    *reinterpret_cast<uint2*>(R1 + px * L.SM + co) = v;
-                                });
+    auto p1_store = [&](int px, int co, uint2 v) {
+        const int r = px / MW, cc = px - r * MW;
+        const int gh = h0 - 1 + r, gw = w0 - 1 + cc;
+        if (!((unsigned)gh < (unsigned)H && (unsigned)gw < (unsigned)W)) v = make_uint2(0, 0);
+        *reinterpret_cast<uint2*>(R1 + px * L.SM + co) = v;
+    };
+    if constexpr (NAP1 > 0)
+        hc_pw_run<T, NK1, NAP1>(R2, L.SD, MH * MW, reinterpret_cast<const T*>(V.pw1w), V.pw1ld, QB1, c3, true, A1,
+                                p1_store);
+    else
+        hc_pw_wide<T, NK1>(R2, L.SD, MH * MW, reinterpret_cast<const T*>(V.pw1w), V.pw1ld, QB1, c3, true, p1_store);
     HcA<NK2, HC_NA> A2;   // pw2's weights, in flight during dw2
     hc_pw_pre<T, NK2, HC_NA>(reinterpret_cast<const T*>(V.pw2w), V.pw2ld, c3, A2);
     // 4. dw2 (opens with the barrier after pw1): P1 (R1) -> D2 (R2) over the TH x TW tile
@@ -345,6 +405,8 @@ __global__ __launch_bounds__(HEAD_CLS_THREADS, 3) void head_cls(const HeadClsArg
     else if (nk1 == 8 && nk2 == 5) hc_body<T, 8, 1, 5>(A, li, hsm);
     else if (nk1 == 4 && nk2 == 4) hc_body<T, 4, HC_NA, 4>(A, li, hsm);
     else if (nk1 == 8 && nk2 == 4) hc_body<T, 8, 1, 4>(A, li, hsm);
+    else if (nk1 == 16 && nk2 == 5) hc_body<T, 16, 0, 5>(A, li, hsm);
+    else if (nk1 == 16 && nk2 == 4) hc_body<T, 16, 0, 4>(A, li, hsm);
 }
 
 // Box tail: each wave takes BOX_DFL_TPW consecutive 32-pixel tiles of a level's flattened
@@ -470,8 +532,8 @@ int launch_box_dfl(int dtype, const BoxDflArgs& a, hipStream_t s) {
 
 int head_cls_lds(int TH, int TW, int C0, int c3, int nc) {
     if (C0 % 64 && C0 > 64) return 0;            // whole 64-channel chunks
-    // instantiated: C0 64 / 128, c3 64 / 80, at most three 32-cout tiles per pointwise conv
-    if (!(C0 == 64 || C0 == 128) || !(c3 == 64 || c3 == 80) || nc > 32 * HC_NA) return 0;
+    // instantiated: C0 64 / 128 / 256, c3 64 / 80, at most three 32-cout tiles per pointwise conv
+    if (!(C0 == 64 || C0 == 128 || C0 == 256) || !(c3 == 64 || c3 == 80) || nc > 32 * HC_NA) return 0;
     // parameter chunks: 10 (C0 + c3) / 4 + 72 <= 4 per thread
     if ((10 * (C0 + c3)) / 4 + 72 > 4 * HEAD_CLS_THREADS) return 0;
     const HcLayout L = hc_layout(TH, TW, C0, c3);
