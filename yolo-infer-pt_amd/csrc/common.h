@@ -154,11 +154,16 @@ struct HeadClsArgs {
     // caller's y = io[1] (B, 4+nc, A) instead of the head tensor (the decode's class part)
     const void* const* io; int A;
 };
-constexpr int HEAD_CLS_THREADS = 256;
+#ifndef YH_HEAD_CLS_THREADS
+#define YH_HEAD_CLS_THREADS 512
+#endif
+// 8-wave workgroups, two per CU (16 waves); 256 = the round-2 4-wave kernel (fragments
+// preloaded a phase ahead), 7 % slower (profiles/r03_ops_hcls_{256,512}.txt)
+constexpr int HEAD_CLS_THREADS = YH_HEAD_CLS_THREADS;
 #ifndef YH_HEAD_CLS_LDS_KB
 #define YH_HEAD_CLS_LDS_KB 80
 #endif
-constexpr int HEAD_CLS_LDS = YH_HEAD_CLS_LDS_KB * 1024;   // 80: two workgroups (8 waves) per CU, 8x16 tiles at 80x80
+constexpr int HEAD_CLS_LDS = YH_HEAD_CLS_LDS_KB * 1024;   // 80: two workgroups (16 waves) per CU, 8x16 tiles at 80x80
 // LDS bytes of a tile's buffers; 0 if it does not fit
 int head_cls_lds(int TH, int TW, int C0, int c3, int nc);
 int launch_head_cls(int dtype, const HeadClsArgs& a, hipStream_t s);

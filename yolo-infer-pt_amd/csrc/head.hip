@@ -39,6 +39,7 @@ template <> struct HMfma<_Float16> {
 };
 
 constexpr int NWV = HEAD_CLS_THREADS / 64;
+constexpr bool HC_UNITS = NWV >= 8;
 
 // the decode's 16-bit exp and division (misc.hip ex<T> / dv<T>): same instructions, same bits
 __device__ __forceinline__ float hx_exp(float x) { return __expf(x); }
@@ -220,16 +221,17 @@ __device__ __forceinline__ void hc_pw_run(const T* src, int ss, int NPX, const T
 template <int NK>
 struct HcA<NK, 0> {};
 
-// Pointwise phase for wide K (NK > 8: the 256-channel 20x20 level's pw1): the work units are
-// (32-pixel B tile, 32-cout A tile) pairs round-robin over the waves, and K runs in 8-block
-// halves, the next half's A (global) and B (LDS) fragments loading while the current half's
-// MFMAs run. One fp32 chain per unit over the 16-channel blocks in ascending order: the same
-// K order, the same bits as hc_pw_run and the per-layer 1x1 conv.
+// Pointwise phase over (32-pixel B tile, 32-cout A tile) work units, round-robin over the
+// waves: the wide-K pw1 (NK > 8: the 256-channel 20x20 level) and, with 8-wave workgroups,
+// every pointwise phase (no fragments held across phases). K runs in pieces of up to 8
+// blocks; with two pieces the next one's A (global) and B (LDS) fragments load while the
+// current one's MFMAs run. One fp32 chain per unit over the 16-channel blocks in ascending
+// order: the same K order, the same bits as hc_pw_run and the per-layer 1x1 conv.
 template <typename T, int NK, typename Store>
-__device__ __forceinline__ void hc_pw_wide(const T* src, int ss, int NPX, const T* w, int wld, const float* bias, int M,
-                                           bool silu_act, Store store) {
-    static_assert(NK % 8 == 0, "whole 8-block halves");
-    constexpr int NH = NK / 8;
+__device__ __forceinline__ void hc_pw_units(const T* src, int ss, int NPX, const T* w, int wld, const float* bias, int M,
+                                            bool silu_act, Store store) {
+    constexpr int KP = NK <= 8 ? NK : 8, NH = NK / KP;
+    static_assert(NK % KP == 0, "whole K pieces");
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const int l32 = lane & 31, h = lane >> 5;
     const int na = (M + 31) >> 5, nb = (NPX + 31) >> 5;
@@ -240,12 +242,12 @@ __device__ __forceinline__ void hc_pw_wide(const T* src, int ss, int NPX, const 
         const int pxc = px < NPX ? px : NPX - 1;
         const T* brow = src + pxc * ss + 8 * h;
         const T* wrow = w + (long long)(a * 32 + l32) * wld + 8 * h;
-        uint4 af[2][8], bf[2][8];
+        uint4 af[NH > 1 ? 2 : 1][KP], bf[NH > 1 ? 2 : 1][KP];
         auto load = [&](int hh, int buf) {
 #pragma unroll
-            for (int kb = 0; kb < 8; ++kb) {
-                af[buf][kb] = *reinterpret_cast<const uint4*>(wrow + (hh * 8 + kb) * 16);
-                bf[buf][kb] = *reinterpret_cast<const uint4*>(brow + (hh * 8 + kb) * 16);
+            for (int kb = 0; kb < KP; ++kb) {
+                af[buf][kb] = *reinterpret_cast<const uint4*>(wrow + (hh * KP + kb) * 16);
+                bf[buf][kb] = *reinterpret_cast<const uint4*>(brow + (hh * KP + kb) * 16);
             }
         };
         load(0, 0);
@@ -256,7 +258,7 @@ __device__ __forceinline__ void hc_pw_wide(const T* src, int ss, int NPX, const 
         for (int hh = 0; hh < NH; ++hh) {
             if (hh + 1 < NH) load(hh + 1, (hh + 1) & 1);
 #pragma unroll
-            for (int kb = 0; kb < 8; ++kb) acc = HMfma<T>::step(af[hh & 1][kb], bf[hh & 1][kb], acc);
+            for (int kb = 0; kb < KP; ++kb) acc = HMfma<T>::step(af[hh & 1][kb], bf[hh & 1][kb], acc);
         }
         if (px < NPX) {
 #pragma unroll
@@ -320,8 +322,11 @@ __device__ __forceinline__ void hc_body(const HeadClsArgs& A, int li, char* hsm)
         }
     }
     const T* x = reinterpret_cast<const T*>(V.x);
-    HcA<NK1, NAP1> A1;   // pw1's weights, in flight while the input tile loads
-    if constexpr (NAP1 > 0) hc_pw_pre<T, NK1, NAP1>(reinterpret_cast<const T*>(V.pw1w), V.pw1ld, c3, A1);
+    // 8-wave workgroups run every pointwise phase as (B tile, A tile) units with no
+    // fragments held across phases (HC_UNITS); 4-wave ones preload them a phase ahead
+    constexpr int P1 = HC_UNITS ? 0 : NAP1;
+    HcA<NK1, P1> A1;   // pw1's weights, in flight while the input tile loads
+    if constexpr (P1 > 0) hc_pw_pre<T, NK1, P1>(reinterpret_cast<const T*>(V.pw1w), V.pw1ld, c3, A1);
 
     // 1-2. per 64-channel chunk: input tile with a 2-pixel halo (zeros outside the image =
     //      dw1's zero padding) -> R1, then dw1 of the chunk over the MH x MW mid region -> R2
@@ -353,49 +358,63 @@ __device__ __forceinline__ void hc_body(const HeadClsArgs& A, int li, char* hsm)
         if (!((unsigned)gh < (unsigned)H && (unsigned)gw < (unsigned)W)) v = make_uint2(0, 0);
         *reinterpret_cast<uint2*>(R1 + px * L.SM + co) = v;
     };
-    if constexpr (NAP1 > 0)
-        hc_pw_run<T, NK1, NAP1>(R2, L.SD, MH * MW, reinterpret_cast<const T*>(V.pw1w), V.pw1ld, QB1, c3, true, A1,
-                                p1_store);
+    if constexpr (P1 > 0)
+        hc_pw_run<T, NK1, P1>(R2, L.SD, MH * MW, reinterpret_cast<const T*>(V.pw1w), V.pw1ld, QB1, c3, true, A1,
+                              p1_store);
     else
-        hc_pw_wide<T, NK1>(R2, L.SD, MH * MW, reinterpret_cast<const T*>(V.pw1w), V.pw1ld, QB1, c3, true, p1_store);
-    HcA<NK2, HC_NA> A2;   // pw2's weights, in flight during dw2
-    hc_pw_pre<T, NK2, HC_NA>(reinterpret_cast<const T*>(V.pw2w), V.pw2ld, c3, A2);
+        hc_pw_units<T, NK1>(R2, L.SD, MH * MW, reinterpret_cast<const T*>(V.pw1w), V.pw1ld, QB1, c3, true, p1_store);
+    constexpr int P2 = HC_UNITS ? 0 : HC_NA;
+    HcA<NK2, P2> A2;   // pw2's weights, in flight during dw2
+    if constexpr (P2 > 0) hc_pw_pre<T, NK2, P2>(reinterpret_cast<const T*>(V.pw2w), V.pw2ld, c3, A2);
     // 4. dw2 (opens with the barrier after pw1): P1 (R1) -> D2 (R2) over the TH x TW tile
     hc_dw<T>(R1, MW, L.SM, R2, TH, TW, L.SM, 0, c3, PW2, c3, PB2);
     // 5. pw2: D2 (R2) -> P2 (R1)
-    hc_pw_run<T, NK2, HC_NA>(R2, L.SM, TH * TW, reinterpret_cast<const T*>(V.pw2w), V.pw2ld, QB2, c3, true, A2,
-                                 [&](int px, int co, uint2 v) { *reinterpret_cast<uint2*>(R1 + px * L.SM + co) = v; });
-    HcA<NK2, HC_NA> A3;   // pw3's weights: issued once pw2's are dead
-    hc_pw_pre<T, NK2, HC_NA>(reinterpret_cast<const T*>(V.pw3w), V.pw3ld, A.nc, A3);
+    auto p2_store = [&](int px, int co, uint2 v) { *reinterpret_cast<uint2*>(R1 + px * L.SM + co) = v; };
+    if constexpr (P2 > 0)
+        hc_pw_run<T, NK2, P2>(R2, L.SM, TH * TW, reinterpret_cast<const T*>(V.pw2w), V.pw2ld, QB2, c3, true, A2,
+                              p2_store);
+    else
+        hc_pw_units<T, NK2>(R2, L.SM, TH * TW, reinterpret_cast<const T*>(V.pw2w), V.pw2ld, QB2, c3, true, p2_store);
+    HcA<NK2, P2> A3;   // pw3's weights: issued once pw2's are dead
+    if constexpr (P2 > 0) hc_pw_pre<T, NK2, P2>(reinterpret_cast<const T*>(V.pw3w), V.pw3ld, A.nc, A3);
     // 6. pw3: P2 (R1) -> class logits in the head tensor, or (direct mode) their sigmoid in
     //    the caller's y, one row per class (the decode's class part: logit rounded first)
     T* y = reinterpret_cast<T*>(V.y);
+    auto pw3 = [&](auto store) {
+        if constexpr (P2 > 0)
+            hc_pw_run<T, NK2, P2>(R1, L.SM, TH * TW, reinterpret_cast<const T*>(V.pw3w), V.pw3ld, QB3, A.nc, false, A3,
+                                  store);
+        else
+            hc_pw_units<T, NK2>(R1, L.SM, TH * TW, reinterpret_cast<const T*>(V.pw3w), V.pw3ld, QB3, A.nc, false, store);
+    };
     if (A.io)
-        hc_pw_run<T, NK2, HC_NA>(R1, L.SM, TH * TW, reinterpret_cast<const T*>(V.pw3w), V.pw3ld, QB3, A.nc, false,
-                                 A3, [&](int px, int co, uint2 v) {
-                                     const int r = px / TW, cc = px - r * TW;
-                                     const int gh = h0 + r, gw = w0 + cc;
-                                     if ((unsigned)gh < (unsigned)H && (unsigned)gw < (unsigned)W) {
-                                         T* col = reinterpret_cast<T*>(const_cast<void*>(A.io[1])) +
-                                                  ((long long)n * (4 + A.nc) + 4 + co) * A.A + V.aoff + gh * W + gw;
-                                         const T* o = reinterpret_cast<const T*>(&v);
+        pw3([&](int px, int co, uint2 v) {
+            const int r = px / TW, cc = px - r * TW;
+            const int gh = h0 + r, gw = w0 + cc;
+            if ((unsigned)gh < (unsigned)H && (unsigned)gw < (unsigned)W) {
+                T* col = reinterpret_cast<T*>(const_cast<void*>(A.io[1])) +
+                         ((long long)n * (4 + A.nc) + 4 + co) * A.A + V.aoff + gh * W + gw;
+                const T* o = reinterpret_cast<const T*>(&v);
 #pragma unroll
-                                         for (int e = 0; e < 4; ++e)
-                                             col[(long long)e * A.A] = fromf<T>(hx_div(1.0f, 1.0f + hx_exp(-tof(o[e]))));
-                                     }
-                                 });
+                for (int e = 0; e < 4; ++e) col[(long long)e * A.A] = fromf<T>(hx_div(1.0f, 1.0f + hx_exp(-tof(o[e]))));
+            }
+        });
     else
-        hc_pw_run<T, NK2, HC_NA>(R1, L.SM, TH * TW, reinterpret_cast<const T*>(V.pw3w), V.pw3ld, QB3, A.nc, false,
-                                 A3, [&](int px, int co, uint2 v) {
-                                     const int r = px / TW, cc = px - r * TW;
-                                     const int gh = h0 + r, gw = w0 + cc;
-                                     if ((unsigned)gh < (unsigned)H && (unsigned)gw < (unsigned)W)
-                                         *reinterpret_cast<uint2*>(y + (((long long)n * H + gh) * W + gw) * V.ldy + co) = v;
-                                 });
+        pw3([&](int px, int co, uint2 v) {
+            const int r = px / TW, cc = px - r * TW;
+            const int gh = h0 + r, gw = w0 + cc;
+            if ((unsigned)gh < (unsigned)H && (unsigned)gw < (unsigned)W)
+                *reinterpret_cast<uint2*>(y + (((long long)n * H + gh) * W + gw) * V.ldy + co) = v;
+        });
 }
 
+#if YH_HEAD_CLS_THREADS >= 512
+#define HC_BOUNDS __launch_bounds__(HEAD_CLS_THREADS) __attribute__((amdgpu_waves_per_eu(4, 4)))
+#else
+#define HC_BOUNDS __launch_bounds__(HEAD_CLS_THREADS, 3)
+#endif
 template <typename T>
-__global__ __launch_bounds__(HEAD_CLS_THREADS, 3) void head_cls(const HeadClsArgs A) {
+__global__ HC_BOUNDS void head_cls(const HeadClsArgs A) {
     extern __shared__ __attribute__((aligned(16))) char hsm[];
     int li = 0;
     if (A.nlv > 1 && (int)blockIdx.x >= A.lv[1].wg0) li = 1;
