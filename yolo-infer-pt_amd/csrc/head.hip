@@ -61,7 +61,10 @@ __device__ __forceinline__ void hc_glds(const void* src, unsigned lds_addr) {
 // load in flight (vmcnt(0)), which would drain the weight loads issued ahead of a phase.
 __device__ __forceinline__ void hc_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 constexpr int HC_CK = 64;    // input channels staged per pass (the first depthwise conv's chunk)
-constexpr int HC_RB = 4;     // output rows per depthwise item (register sliding window)
+#ifndef YH_HC_RB
+#define YH_HC_RB 4
+#endif
+constexpr int HC_RB = YH_HC_RB;   // output rows per depthwise item (register sliding window)
 
 // LDS of one tile: region 1 = the input chunk (XH x XW x min(C0, HC_CK)), later the first /
 // second pointwise outputs; region 2 = the first / second depthwise outputs
