@@ -125,18 +125,24 @@ def pmc_traffic(cls, args):
     """HBM bytes per launch of kernel family `cls` from the committed rocprofv3 PMC summary
     (FETCH_SIZE / WRITE_SIZE passes over tools/pmc_run.py, corrected per the gfx950 guide by
     tools/pmc_traffic.py); bench.py cannot collect PMC counters from inside its own process.
-    None unless the summary was collected on this bench's configuration."""
-    try:
-        with open(PMC_SUMMARY) as f:
-            rec = json.load(f)
-        cfg = rec.get("config", {"variant": "n", "size": 640, "batch": 32, "dtype": "bf16"})
-        if (cfg["variant"], cfg["size"], cfg["batch"], cfg["dtype"]) != (args.variant, args.size, args.batch, args.dtype):
-            return None, None
-        fam = rec["family"][cls]
-        return round(fam["traffic_per_launch"]), (f"{os.path.relpath(PMC_SUMMARY, ROOT)}: {rec['source']}; "
-                                                  f"{rec['corrections']}; {fam['traffic_over_alg']:.2f}x algorithmic")
-    except (OSError, KeyError, ValueError):
-        return None, None
+    profiles/pmc_traffic_latest.json (the headline configuration) or, for the other configs,
+    profiles/pmc_traffic_<variant>_<size>_b<batch>_<dtype>.json (tools/pmc_config.sh).
+    None unless a summary was collected on this bench's configuration."""
+    want = (args.variant, args.size, args.batch, args.dtype)
+    per_cfg = os.path.join(ROOT, "profiles", "pmc_traffic_%s_%d_b%d_%s.json" % want)
+    for path in (PMC_SUMMARY, per_cfg):
+        try:
+            with open(path) as f:
+                rec = json.load(f)
+            cfg = rec.get("config", {"variant": "n", "size": 640, "batch": 32, "dtype": "bf16"})
+            if (cfg["variant"], cfg["size"], cfg["batch"], cfg["dtype"]) != want:
+                continue
+            fam = rec["family"][cls]
+            return round(fam["traffic_per_launch"]), (f"{os.path.relpath(path, ROOT)}: {rec['source']}; "
+                                                      f"{rec['corrections']}; {fam['traffic_over_alg']:.2f}x algorithmic")
+        except (OSError, KeyError, ValueError):
+            continue
+    return None, None
 
 
 def _cpu_model():

@@ -26,15 +26,17 @@ def main():
     v = os.environ.get("YH_VARIANT", "n")
     size = int(os.environ.get("YH_SIZE", "640"))
     B = int(os.environ.get("YH_BATCH", "32"))
+    dname = os.environ.get("YH_DTYPE", "bf16")
+    dt = {"bf16": torch.bfloat16, "fp16": torch.float16}[dname]
     from nets import nn
     torch.manual_seed(0)
     model = getattr(nn, f"yolo_v11_{v}")(80)
     model.load_state_dict(synth.synth_state_dict(model.state_dict(), seed=0))
     model.eval()
     dev = torch.device("cuda", 0)
-    eng = Engine(*model._yh_arch, dev, torch.bfloat16)
+    eng = Engine(*model._yh_arch, dev, dt)
     eng.load_module(model)
-    x = synth.synth_scenes(B, size, size, seed=100).to(dev, torch.bfloat16)
+    x = synth.synth_scenes(B, size, size, seed=100).to(dev, dt)
     eng.forward(x)          # autotune (many candidate launches)
     eng.set_graph(False)
     y = eng.forward(x)
@@ -47,7 +49,7 @@ def main():
     out = os.environ.get("YH_OPS_OUT")
     if out:
         with open(out, "w") as f:
-            json.dump(dict(config=dict(variant=v, size=size, batch=B, dtype="bf16"),
+            json.dump(dict(config=dict(variant=v, size=size, batch=B, dtype=dname),
                            ops=[dict(label=o["label"], cls=o["cls"], bytes=o["bytes"], kernel=o["kernel"])
                                 for o in (u["ops"][0] for u in eng.units(B, size, size))]), f)
     print("pmc workload done", flush=True)
