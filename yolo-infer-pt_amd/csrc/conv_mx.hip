@@ -1003,6 +1003,8 @@ std::vector<MxPlan> mx_candidates(const MxShape& sh, int num_cus) {
             add(2, 2, 1, 4, ncb);
             add(1, 4, 1, 4, ncb);
             if (sh.cout > 64) add(2, 2, 2, 2, ncb);
+            // 256-cout slices for wide layers: the input patch is read by half as many slices
+            if (sh.cout >= 512) add(2, 2, 4, 2, ncb);
         }
     }
     // resident-weight per-wave kernels (instantiated set, see launch_mxr_cfg)
@@ -1172,6 +1174,7 @@ int launch_mx_cfg(const MxPlan& pl, const MxArgs& a, hipStream_t s) {
     YH_MX(1, 4, 1, 4)
     YH_MX(1, 2, 1, 4)
     YH_MX(2, 2, 2, 2)
+    YH_MX(2, 2, 4, 2)
 #undef YH_MX
     return (int)hipErrorInvalidValue;
 }
