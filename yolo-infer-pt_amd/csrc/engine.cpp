@@ -1183,10 +1183,10 @@ struct Net {
         int l0 = 0;
         while (!op.hlv[l0]) ++l0;
         a.c3 = convs[op.hc[l0][1]].cout;
-        // workgroup order: the 20x20 level first (four input-channel chunks per tile, the
-        // longest workgroups), then 80x80 and 40x40
+        // workgroup order: levels 0, 1, 2 (issuing the 20x20 level first was 1.5-3 us slower,
+        // profiles/r03_ops_hcls_order.txt)
         int lvls[3], nl = 0;
-        for (int l : {2, 0, 1})
+        for (int l = 0; l < 3; ++l)
             if (op.hlv[l]) lvls[nl++] = l;
         for (int k = 0; k < nl; ++k) {
             const int l = lvls[k];
