@@ -206,6 +206,23 @@ def cpu_baseline(args, runs=3):
                        f"{threads} threads, torch.inference_mode()")
 
 
+def launch_ranks(n, argv):
+    """`bench.py --gpus N` (N > 1) started without a launcher: run N ranks, one per GPU, under
+    torch.distributed.run as child processes and return its exit code. The reference's own
+    multi-process entry is env-driven under a launcher (main.py:338-344, main.sh:1-2); here the
+    bench provides the launcher itself. This parent makes no GPU call (it only imports torch and
+    counts devices, which does not initialise HIP), so the ranks start from a clean process."""
+    import socket
+    import subprocess
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__), *argv]
+    log(f"bench: launching {n} ranks: {' '.join(cmd[1:])}")
+    return subprocess.call(cmd, env=dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0"))
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -228,7 +245,15 @@ def main():
                     help="distinct input batches the timed steps cycle through (> 256 MB of MALL in total)")
     ap.add_argument("--serial", action="store_true",
                     help="run forward and NMS back to back on one stream (no batch-to-batch overlap)")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="no HIP: gloo on the CPU and a stub step (the gather of empty detection buffers); "
+                         "checks the launcher, rank layout, timing and JSON line without a GPU")
     args = ap.parse_args()
+
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        if not args.dry_run and torch.cuda.device_count() < args.gpus:
+            raise SystemExit(f"bench.py --gpus {args.gpus}: only {torch.cuda.device_count()} GPU(s) visible")
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -236,6 +261,10 @@ def main():
     # launched by torch.distributed.run (RANK + MASTER_ADDR set): a process group even at
     # world size 1, so the RCCL gather of the results runs on the device in every such run
     dist = world > 1 or ("RANK" in os.environ and "MASTER_ADDR" in os.environ)
+    if "WORLD_SIZE" in os.environ and args.gpus != world:
+        log(f"bench: --gpus {args.gpus} but the launcher started {world} rank(s); n_gpus = {world}")
+    if args.dry_run:
+        return dry_run(args, rank, world, dist)
     if dist:
         torch.cuda.set_device(local)
         torch.distributed.init_process_group("nccl", device_id=torch.device("cuda", local))
@@ -357,6 +386,44 @@ def main():
                        f"last step rank-0 rows match: {gather_check}") if dist else None,
         }
         print(json.dumps(rec), flush=True)
+    if dist:
+        torch.distributed.barrier()
+        torch.distributed.destroy_process_group()
+
+
+def dry_run(args, rank, world, dist):
+    """The multi-rank skeleton of main() without HIP: gloo process group, a stub step that gathers
+    an empty (B, 300, 6) detection buffer to rank 0, the same barrier / max-over-ranks timing and
+    one JSON line on rank 0 (tests/test_bench_launch.py runs it at N = 2 on the CPU)."""
+    from yolo_hip.dist import Gather
+    if dist:
+        torch.distributed.init_process_group("gloo")
+    B = args.batch
+    gather = Gather(B, 300, "cpu", rank, world, slots=2)
+    dets = torch.zeros((B, 300, 6))
+    counts = torch.full((B,), rank, dtype=torch.int32)
+    for _ in range(args.warmup):
+        gather(dets, counts)
+    if dist:
+        torch.distributed.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        got = gather(dets, counts)
+    if dist:
+        torch.distributed.barrier()
+    elapsed = time.perf_counter() - t0
+    if dist:
+        t = torch.tensor([elapsed], dtype=torch.float64)
+        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+        elapsed = t.item()
+    if rank == 0:
+        ranks_seen = [int(p[0, -1].item()) for p in got]
+        print(json.dumps({"metric": "dry run (no HIP)", "value": round(B * world * args.steps / elapsed, 2),
+                          "unit": "images/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+                          "ms_per_step": round(elapsed / args.steps * 1e3, 4), "higher_is_better": True,
+                          "scaling": "weak", "vs_baseline": None, "dry_run": True, "ranks_gathered": ranks_seen,
+                          "config": {"per_gpu_batch": B, "global_batch": B * world,
+                                     "parallelism": f"dp{world}"}}), flush=True)
     if dist:
         torch.distributed.barrier()
         torch.distributed.destroy_process_group()

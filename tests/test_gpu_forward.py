@@ -262,3 +262,38 @@ def test_x_1280_c5_bench_shape(gpu):
     want = g["dets"][:int(g["counts"][0])]
     m50, miou = detection_match(dets[0, :counts[0]].cpu().numpy(), want)
     print(f"v11_x@1280 bf16 b16 detections: match@0.5 {m50:.3f} mean IoU {miou:.4f}")
+    assert m50 >= 0.99 and miou >= 0.95, (m50, miou)
+
+
+def test_n_bf16_c2_bench_shape(gpu):
+    """C2's own configuration (v11_n, bf16, 640x640, batch 32, the headline bench), image 0 = the
+    golden's input: the per-shape tuner's plans and the batch-32 fused-kernel choices (c3k,
+    head_cls, K-split) give images 0, 17 and 31 exactly their batch-1 outputs, image 0 is within
+    the reference's own bf16 deviation of the float64 golden (forward_n_640_b1.npz), and its
+    post-NMS detections match the golden's as well as the reference algorithm run in bf16 does."""
+    from _util import detection_match, oracle_for
+    from oracle import nms as onms
+    from yolo_hip.engine import nms
+    g = load_golden(golden_name("n", 640, 1))
+    x0 = synth.synth_scenes(1, 640, 640, seed=GOLDEN_INPUT_SEED)
+    rest = synth.synth_scenes(31, 640, 640, seed=41)
+    x = torch.cat([x0, rest]).to(gpu, torch.bfloat16)
+    eng = _engine(make_model("n"), torch.bfloat16, gpu)
+    y = eng.forward(x).clone()
+    assert torch.isfinite(y.float()).all()
+    for i in (0, 17, 31):
+        y1 = eng.forward(x[i:i + 1].contiguous())
+        assert torch.equal(y1[0], y[i]), f"image {i}: batch-32 plans differ from batch-1"
+    ref = g["y"].astype(np.float64)
+    d = np.abs(y[:1].float().cpu().double().numpy() - ref)
+    fl = [float(v) for v in g["dev_bf16"]]
+    print(f"v11_n@640 bf16 b32 image 0: box max {d[:, :4].max():.3g} mean {d[:, :4].mean():.3g} (reference "
+          f"{fl[0]:.3g} / {fl[1]:.3g}); cls max {d[:, 4:].max():.3g} mean {d[:, 4:].mean():.3g}")
+    half_bars(d, fl[0], fl[1], fl[2], fl[3])
+    want = onms.non_max_suppression(g["y"].astype(np.float32))[0]
+    dets, counts = nms(y[:1])
+    m50, miou = detection_match(dets[0, :counts[0]].cpu().numpy(), want)
+    ref_half = oracle_for("n", torch.bfloat16)(x0.to(torch.bfloat16)).float().numpy()
+    r50, riou = detection_match(onms.non_max_suppression(ref_half, half=torch.bfloat16)[0], want)
+    print(f"v11_n@640 bf16 b32 detections: match@0.5 {m50:.3f} mean IoU {miou:.4f} (reference bf16 {r50:.3f} / {riou:.4f})")
+    assert m50 >= min(0.99, r50) - 0.03 and miou >= min(0.99, riou) - 0.03

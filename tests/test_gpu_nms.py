@@ -125,3 +125,18 @@ def test_dropin_non_max_suppression(gpu):
     out = non_max_suppression(y)
     assert isinstance(out, list) and len(out) == 1 and out[0].device == y.device
     _assert_same([out[0].cpu().numpy()], _unpack(g["counts"], g["dets"]))
+
+
+@pytest.mark.parametrize("iou", [-0.1, -0.0, -1e-30])
+def test_negative_iou_threshold_vs_oracle(gpu, iou):
+    """with iou_threshold < 0 a disjoint pair (IoU 0 > thr) suppresses too, across
+    classes, so the same-class shortcut must not apply (torchvision's greedy contract)."""
+    rng = np.random.default_rng(11)
+    B, A, nc = 2, 900, 80
+    y = np.empty((B, 4 + nc, A), np.float32)
+    y[:, 0:2] = rng.uniform(0, 640, size=(B, 2, A))
+    y[:, 2:4] = rng.uniform(8, 60, size=(B, 2, A))
+    y[:, 2:4, ::50] = 0.0   # zero-area boxes: 0 / 0 union, NaN IoU never suppresses
+    y[:, 4:] = (1 / (1 + np.exp(-rng.normal(-5, 2.5, size=(B, nc, A))))).astype(np.float32)
+    want = onms.non_max_suppression(y, 0.001, iou, 300, 30000)
+    _assert_same(_gpu_nms(torch.from_numpy(y), gpu, iou_threshold=iou), want)

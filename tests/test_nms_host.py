@@ -82,3 +82,18 @@ def test_thread_count_does_not_change_results():
     d1, c1 = nms_host(y, threads=1)
     d8, c8 = nms_host(y, threads=8)
     assert torch.equal(c1, c8) and torch.equal(d1, d8)
+
+
+@pytest.mark.parametrize("iou", [-0.1, -0.0])
+def test_negative_iou_threshold_vs_oracle(iou):
+    """iou_threshold < 0: disjoint pairs (IoU 0) suppress too, across classes; zero-area boxes
+    (NaN IoU) never do."""
+    rng = np.random.default_rng(11)
+    B, A, nc = 2, 900, 80
+    y = np.empty((B, 4 + nc, A), np.float32)
+    y[:, 0:2] = rng.uniform(0, 640, size=(B, 2, A))
+    y[:, 2:4] = rng.uniform(8, 60, size=(B, 2, A))
+    y[:, 2:4, ::50] = 0.0
+    y[:, 4:] = (1 / (1 + np.exp(-rng.normal(-5, 2.5, size=(B, nc, A))))).astype(np.float32)
+    _assert_same(_host_nms(torch.from_numpy(y), iou_threshold=iou),
+                 onms.non_max_suppression(y, 0.001, iou, 300, 30000))

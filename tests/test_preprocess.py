@@ -98,29 +98,101 @@ def _write_set(root, shapes):
         fn = os.path.join(root, "images", "val", f"{i:03d}.png")
         Image.fromarray(np.ascontiguousarray(rgb)).save(fn)
         with open(os.path.join(root, "labels", "val", f"{i:03d}.txt"), "w") as f:
-            if i % 3 != 2:   # every third image has no labels
-                f.write(f"{i % 80} 0.5 0.5 0.25 0.4\n3 0.2 0.3 0.1 0.1\n")
+            for row in _labels_of(i):   # every third image has no labels
+                f.write(" ".join(str(v) for v in row) + "\n")
         imgs.append(np.ascontiguousarray(rgb[:, :, ::-1]))
         files.append(fn)
     return files, imgs
 
 
 def test_dataset_eval_items(tmp_path):
+    """dataset.py:30-90 (augment=False): (sample, cls, box, zeros(n)); the sample is the letterbox
+    (load_image + resize + CHW/RGB), the labels are moved onto the letterboxed canvas."""
     from utils import dataset
     shapes = [(480, 640), (640, 427), (300, 300), (1280, 960), (200, 640)]
     files, imgs = _write_set(str(tmp_path), shapes)
     ds = dataset.Dataset(files, 640, {}, augment=False)
     assert len(ds) == len(files)
     for i in range(len(ds)):
-        sample, (h0, w0) = ds[i]
-        assert (h0, w0) == shapes[i]
+        sample, cls, box, idx = ds[i]
         assert sample.dtype == torch.uint8 and sample.shape == (3, 640, 640)
         assert np.array_equal(sample.numpy(), opre.letterbox(imgs[i], 640))
         # the reference's two-step route: load_image, resize (pad), CHW + BGR->RGB
-        im, _ = ds.load_image(i)
+        im, (h0, w0) = ds.load_image(i)
+        assert (h0, w0) == shapes[i]
         padded, ratio, pad = dataset.resize(im, 640, False)
         assert ratio == (1.0, 1.0)
         assert np.array_equal(np.ascontiguousarray(padded.transpose(2, 0, 1)[::-1]), sample.numpy())
         assert np.array_equal(ds.raw(i).numpy(), imgs[i])
+        # labels: class column + normalised (cx, cy, w, h) on the 640 canvas
+        want = _expected_targets(shapes[i], _labels_of(i), 640)
+        assert cls.shape == (len(want), 1) and box.shape == (len(want), 4) and idx.shape == (len(want),)
+        assert torch.equal(idx, torch.zeros(len(want)))
+        if len(want):
+            np.testing.assert_array_equal(cls.numpy()[:, 0], want[:, 0])
+            np.testing.assert_allclose(box.numpy(), want[:, 1:], rtol=0, atol=2e-6)
     with pytest.raises(NotImplementedError):
         dataset.Dataset(files, 640, {}, augment=True)
+
+
+def _labels_of(i):
+    return [] if i % 3 == 2 else [(i % 80, 0.5, 0.5, 0.25, 0.4), (3, 0.2, 0.3, 0.1, 0.1)]
+
+
+def _expected_targets(shape, labels, S):
+    """Restatement of the label path of dataset.py:45-61 for eval: the image is scaled by
+    S / max(h, w) (int sizes, load_image), never enlarged, centred with a zero border (resize);
+    a normalised label maps to pixels on that canvas, is clipped to [0, S - 1e-3] and
+    re-normalised by S. float64 here, float32 in the loader."""
+    h0, w0 = shape
+    r0 = S / max(h0, w0)
+    h, w = (int(h0 * r0), int(w0 * r0)) if r0 != 1 else (h0, w0)
+    r = min(S / h, S / w, 1.0)
+    dw, dh = (S - round(w * r)) / 2, (S - round(h * r)) / 2
+    out = []
+    for c, cx, cy, bw, bh in labels:   # file order (numpy.unique's sorted order only when rows repeat)
+        x1 = min(max(r * w * (cx - bw / 2) + dw, 0), S - 1e-3)
+        x2 = min(max(r * w * (cx + bw / 2) + dw, 0), S - 1e-3)
+        y1 = min(max(r * h * (cy - bh / 2) + dh, 0), S - 1e-3)
+        y2 = min(max(r * h * (cy + bh / 2) + dh, 0), S - 1e-3)
+        out.append((c, (x1 + x2) / 2 / S, (y1 + y2) / 2 / S, (x2 - x1) / S, (y2 - y1) / S))
+    return np.array(out, dtype=np.float64).reshape(-1, 5)
+
+
+def test_load_label_rules(tmp_path):
+    """dataset.py:195-236: duplicate rows dropped, malformed label files and tiny images skipped,
+    a missing label file gives no labels."""
+    from PIL import Image
+    from utils import dataset
+    root = str(tmp_path)
+    os.makedirs(os.path.join(root, "images", "v"))
+    os.makedirs(os.path.join(root, "labels", "v"))
+    names = ["dup", "bad", "tiny", "nolabel"]
+    files = []
+    for n in names:
+        fn = os.path.join(root, "images", "v", n + ".png")
+        size = (8, 8) if n == "tiny" else (32, 24)
+        Image.fromarray(np.zeros((size[1], size[0], 3), dtype=np.uint8)).save(fn)
+        files.append(fn)
+    with open(os.path.join(root, "labels", "v", "dup.txt"), "w") as f:
+        f.write("1 0.5 0.5 0.2 0.2\n0 0.1 0.1 0.1 0.1\n1 0.5 0.5 0.2 0.2\n")
+    with open(os.path.join(root, "labels", "v", "bad.txt"), "w") as f:
+        f.write("1 0.5 0.5 1.2 0.2\n")
+    got = dataset.Dataset.load_label(files)
+    assert list(got) == [files[0], files[3]]
+    np.testing.assert_array_equal(got[files[0]], np.array([[0, .1, .1, .1, .1], [1, .5, .5, .2, .2]], np.float32))
+    assert got[files[3]].shape == (0, 5)
+
+
+def test_collate_fn_targets():
+    """dataset.py:178-193: labels concatenated, 'idx' = the image's position in the batch."""
+    from utils import dataset
+    items = []
+    for n in (2, 0, 3):
+        items.append((torch.full((3, 4, 4), n, dtype=torch.uint8), torch.arange(n, dtype=torch.float32)[:, None],
+                      torch.rand(n, 4), torch.zeros(n)))
+    x, t = dataset.Dataset.collate_fn(items)
+    assert x.shape == (3, 3, 4, 4) and x[2, 0, 0, 0] == 3
+    assert t['idx'].tolist() == [0, 0, 2, 2, 2]
+    assert t['cls'][:, 0].tolist() == [0, 1, 0, 1, 2]
+    assert torch.equal(t['box'], torch.cat([it[2] for it in items]))

@@ -303,7 +303,11 @@ struct Net {
         conv1(p + ".conv3", full(t), 2 * h, out_ch, ACT_SILU, out);
         // 16-bit handles: the whole block as one launch (c3k.hip) at shapes whose image fits
         // a workgroup's LDS (ensure_plan picks it or the seven launches above per shape)
-        if (dtype != F32 && opt.fuse && opt.c3k && in_ch == 128 && out_ch == 128 && x.C == 128) {
+        // c3k.hip moves 8 channels per 16-byte access at ptr(view) + 8 h: both views must start
+        // on an 8-channel boundary (slice() enforces it today; checked here so the op never
+        // depends on that)
+        if (dtype != F32 && opt.fuse && opt.c3k && in_ch == 128 && out_ch == 128 && x.C == 128 &&
+            x.coff % 8 == 0 && out.coff % 8 == 0) {
             Op op;
             op.kind = OP_C3K;
             op.label = p;

@@ -437,8 +437,9 @@ __device__ void nms_batch(NmsSmem& S, const NmsArgs& p, const T* y, float* dets,
                 hi = fmaxf(hi, S.whi[w]);
                 fin &= S.wfin[w] != 0;
             }
-            // classes separable over the kept set and this sub-batch: test same-class pairs only
-            const bool sep = fin && p.max_wh > 0.0f && p.max_wh < 3.0e38f && hi - lo <= 0.5f * p.max_wh;
+            // classes separable over the kept set and this sub-batch: test same-class pairs only.
+            // Only for thresholds >= 0: with thr < 0 a disjoint pair (IoU 0) still suppresses.
+            const bool sep = th.nonneg && fin && p.max_wh > 0.0f && p.max_wh < 3.0e38f && hi - lo <= 0.5f * p.max_wh;
             bool slow = !th.nonneg;
             {   // 2. suppressed by an already-kept box? 4 threads per entry, 4 kept boxes per step
                 const int e = tid >> 2, part = tid & 3;
@@ -862,7 +863,7 @@ __global__ __launch_bounds__(MASK_T) void nms_mask(const NmsArgs p) {
         }
         const int n = lo, q = t - pre[n];
         const int want = (int)p.state[(long long)n * STW + 1];
-        const bool sep = sep_of(p.state[(long long)n * STW + 7], p.max_wh);
+        const bool sep = th.nonneg && sep_of(p.state[(long long)n * STW + 7], p.max_wh);   // thr < 0: all pairs
         int rb = (int)((sqrtf(8.0f * (float)q + 1.0f) - 1.0f) * 0.5f);
         while (rb * (rb + 1) / 2 > q) --rb;
         while ((rb + 1) * (rb + 2) / 2 <= q) ++rb;
