@@ -261,8 +261,19 @@ def test_x_1280_c5_bench_shape(gpu):
     dets, counts = nms(y[:1])
     want = g["dets"][:int(g["counts"][0])]
     m50, miou = detection_match(dets[0, :counts[0]].cpu().numpy(), want)
-    print(f"v11_x@1280 bf16 b16 detections: match@0.5 {m50:.3f} mean IoU {miou:.4f}")
-    assert m50 >= 0.99 and miou >= 0.95, (m50, miou)
+    # bar: the reference algorithm in bf16 on the CPU (oracle forward + NMS) matches 0.73 / 0.59 of
+    # the float64 golden's top 100, and 0.67-0.75 / 0.54-0.59 when ~0.01 % of the bf16 input
+    # values move by one ulp (tests/golden/x1280_bf16_ref_match.json, oracle/make_x1280_half_match.py):
+    # bf16 v11_x at 1280 is chaotic with the synthetic weights. The device must do no worse than
+    # the worst of those equally valid bf16 runs.
+    import json
+    import os
+    with open(os.path.join(os.path.dirname(__file__), "golden", "x1280_bf16_ref_match.json")) as f:
+        ref = json.load(f)["bf16"]
+    print(f"v11_x@1280 bf16 b16 detections: match@0.5 {m50:.3f} mean IoU {miou:.4f} (reference bf16 "
+          f"{ref['match50']:.3f} / {ref['mean_iou']:.3f}, 1-ulp spread {min(ref['perturbed_match50']):.2f}-"
+          f"{max(ref['perturbed_match50']):.2f})")
+    assert m50 >= min(ref["perturbed_match50"]) and miou >= min(ref["perturbed_mean_iou"]), (m50, miou)
 
 
 def test_n_bf16_c2_bench_shape(gpu):
