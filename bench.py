@@ -97,7 +97,7 @@ def roofline(eng, args, batch, prof_steps, x, y):
                         "on v_mfma_f32_32x32x16, LDS-DMA patch staging, plan autotuned per layer")
                 if args.dtype != "fp32" else "dense 3x3 convs: conv_gemm (fp32 FMA implicit GEMM)",
                 timing="HIP events around each launch on the forward's stream, eager (one forward at a time); "
-                       "profiles/r02_fwd_trace_ops.txt holds the rocprofv3 per-dispatch trace of the same "
+                       f"{TRACE_PROFILE} holds the rocprofv3 per-dispatch trace of the same "
                        "forwards replayed as graphs (tools/fwd_trace.py + tools/trace_ops.py)",
                 launches_per_step=dom["launches"],
                 avg_launch_us=round(dom["ms"] * 1e3 / dom["launches"], 2),
@@ -119,6 +119,7 @@ def roofline(eng, args, batch, prof_steps, x, y):
 
 
 PMC_SUMMARY = os.path.join(ROOT, "profiles", "pmc_traffic_latest.json")
+TRACE_PROFILE = "profiles/r04_fwd_trace_ops.txt"   # rocprofv3 per-dispatch trace of this round's library
 
 
 def pmc_traffic(cls, args):

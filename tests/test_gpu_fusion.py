@@ -140,3 +140,54 @@ def test_head_cls_wide_level_equals_per_layer_launches(gpu, dtype, batch, h, w):
     assert len(lp) - len(lf) == 6
     assert torch.isfinite(yf.float()).all()
     assert torch.equal(yf, yp), (yf.float() - yp.float()).abs().max().item()
+
+
+@pytest.mark.parametrize("variant,dtype,batch,size", [("n", torch.bfloat16, 4, 640), ("s", torch.float16, 2, 320),
+                                                      ("x", torch.bfloat16, 1, 1280), ("n", torch.float16, 2, 224)])
+def test_attention_lds_kernel_equals_per_wave_kernel(gpu, variant, dtype, batch, size):
+    """misc.hip psa_attention_lds (K / V staged in LDS once per workgroup, chunks of 256 keys)
+    runs psa_attention_mfma's per-16-key-block arithmetic in the same order: bit-identical, also
+    over several chunks (x at 1280: 1600 tokens) and with a partial last block (224: 49 tokens).
+    YH_ATTN_LDS is read at launch, so each engine captures its own kernel."""
+    model = make_model(variant)
+    x = synth.synth_scenes(batch, size, size, seed=33).to(gpu, dtype)
+    ys = []
+    for v in ("0", "1"):
+        old = os.environ.get("YH_ATTN_LDS")
+        os.environ["YH_ATTN_LDS"] = v
+        try:
+            eng = _engine(model, dtype, gpu, True)
+            ys.append(eng.forward(x).clone())
+            torch.cuda.synchronize()
+        finally:
+            if old is None:
+                del os.environ["YH_ATTN_LDS"]
+            else:
+                os.environ["YH_ATTN_LDS"] = old
+    assert torch.isfinite(ys[0].float()).all()
+    assert torch.equal(ys[0], ys[1])
+
+
+@pytest.mark.parametrize("bands", ["1", "2", "3", "5", "7", "20"])
+def test_c3k_row_bands_equal_per_layer_launches(gpu, bands):
+    """c3k.hip row bands: each image's block is split over `bands` workgroups that recompute the
+    4-row halo of the chain of four 3x3 convs; every split (1 = one workgroup per image, 20 =
+    one row each at 20x20, uneven splits, a last band with no rows) is bit-identical to the
+    seven per-layer launches. YH_C3K_BANDS is read at launch."""
+    model = make_model("n")
+    x = synth.synth_scenes(2, 640, 640, seed=38).to(gpu, torch.bfloat16)
+    plain = _engine(model, torch.bfloat16, gpu, True, YH_C3K="0")
+    yp = plain.forward(x).clone()
+    old = os.environ.get("YH_C3K_BANDS")
+    os.environ["YH_C3K_BANDS"] = bands
+    try:
+        fused = _engine(model, torch.bfloat16, gpu, True)
+        yf = fused.forward(x).clone()
+        torch.cuda.synchronize()
+    finally:
+        if old is None:
+            del os.environ["YH_C3K_BANDS"]
+        else:
+            os.environ["YH_C3K_BANDS"] = old
+    assert [u["cls"] for u in fused.units(2, 640, 640)].count("c3k") == 2
+    assert torch.equal(yf, yp), (yf.float() - yp.float()).abs().max().item()

@@ -1,11 +1,14 @@
 #!/bin/bash
 # A/B of the in-tree library against exp_lib/base (YH_LIB) on one box: optional GPU tests
-# ($TESTS), per-op HIP-event profiles and benches of both, alternating.
+# ($TESTS, -k $KEXPR; a plain test failure does not stop the A/B, a crash / timeout does),
+# per-op HIP-event profiles and benches of both, alternating.
 set -o pipefail
 O=gpurun_out/${1:-ab}; mkdir -p $O
 if [ -n "$TESTS" ]; then
-  timeout -k 10 500 python -u -m pytest $TESTS -x -q --timeout 300 --timeout-method thread > $O/tests.log 2>&1 || { echo TESTS_FAIL; tail -30 $O/tests.log; exit 1; }
-  tail -2 $O/tests.log
+  timeout -k 10 600 python -u -m pytest $TESTS -k "${KEXPR:-not nothing_deselected}" -q --timeout 300 --timeout-method thread > $O/tests.log 2>&1
+  rc=$?
+  tail -3 $O/tests.log
+  if [ $rc -ge 124 ]; then echo "TESTS_CRASH rc=$rc"; tail -30 $O/tests.log; exit 1; fi
 fi
 B=exp_lib/base/libyolo_hip.so
 YH_LIB=$B timeout -k 10 200 python -u tools/op_profile.py n 640 32 bf16 10 > $O/op_base.txt 2>&1 || { echo OPB_FAIL; tail $O/op_base.txt; exit 1; }

@@ -2,7 +2,12 @@
 // the 16-bit handles, on maps small enough to keep a whole image's intermediates in LDS
 // (v11_n: net.p5.1.res_m.0 and fpn.h6.res_m.0 at 20x20, c = 128, h = c / 2 = 64).
 //
-// One workgroup (16 waves) per image; a 32-pixel tile per wave in every phase:
+// One workgroup (16 waves) per band of RB output rows of one image (the launcher cuts each
+// image into `bands` bands so that a batch fills the chip: one workgroup per image used 32 of
+// 256 CUs at batch 32). The chain of four 3x3 convs needs a 4-row halo: a workgroup keeps the
+// rows [r0 - 4, r1 + 4) of its band (clipped to the image) in LDS and each phase computes the
+// rows its successors read (B: halo 3, C: 2, D: 1, E and F: the band itself); pixels outside a
+// phase's rows are neither computed nor written. A 32-pixel tile per wave in every phase:
 //   A   C1 = conv1(x)            1x1 c -> h, + SiLU                   x from HBM -> LDS C1
 //   B   T  = r0.conv1(C1)        3x3 h -> h, + SiLU                   LDS -> LDS
 //   C   C1 = r0.conv2(T) + C1    3x3 h -> h, + SiLU, + residual       in place (nn.py:49)
@@ -23,6 +28,7 @@
 #include "dtypes.h"
 
 #include <algorithm>
+#include <cstdlib>
 
 namespace yh {
 
@@ -86,6 +92,12 @@ __device__ __forceinline__ void ck_act(const f32x16& acc, const float* b, unsign
 
 }  // namespace
 
+// pixels of the largest band region: RB = ceil(H / bands) rows + 4 halo rows on each side
+__host__ __device__ inline int ck_region_px(int H, int W, int bands) {
+    const int rb = (H + bands - 1) / bands;
+    return (rb + 8 < H ? rb + 8 : H) * W;
+}
+
 // parameter image (bytes): fragments [tile][step][64 lanes][16 B], then fp32 biases
 struct CkLayout {
     int w1, w2, wr, w3, b1, b2, br, b3, total;
@@ -114,35 +126,47 @@ __global__ __launch_bounds__(CK_THREADS, 1) void c3k_fused(const C3kArgs A) {
     typedef __attribute__((address_space(3))) char* lds_c;
     const unsigned lds0 = (unsigned)(size_t)(lds_c)sm;
     const int HW = A.H * A.W;
-    char* C1 = sm;                                   // [HW][64] (swizzled chunks)
-    char* TT = sm + HW * CK_PX;                      // [HW][64]; conv3's 32 KB of weights in phase F
-    const int wb_off = HW * CK_PX + (HW * CK_PX > 32 * 1024 ? HW * CK_PX : 32 * 1024);   // two weight halves
+    // band rows [r0, r1) of image n; LDS region rows [ra0, ra1) (the band + its 4-row halo)
+    const int n = blockIdx.x / A.bands, band = blockIdx.x - n * A.bands;
+    const int RB = (A.H + A.bands - 1) / A.bands;
+    const int r0 = band * RB, r1 = min(A.H, r0 + RB);
+    const int ra0 = max(0, r0 - 4), ra1 = min(A.H, r1 + 4);
+    const int NRP = (ra1 - ra0) * A.W;               // region pixels
+    const int RPX = ck_region_px(A.H, A.W, A.bands);   // LDS pixels per region image (the largest band's)
+    char* C1 = sm;                                   // [RPX][64] (swizzled chunks)
+    char* TT = sm + RPX * CK_PX;                     // [RPX][64]
+    const int wb_off = 2 * RPX * CK_PX;              // two weight halves
     char* WB = sm + wb_off;
     char* ZR = WB + 2 * WBH;                         // 128 zero bytes (out-of-image taps)
     const float* BI = reinterpret_cast<const float*>(ZR + 128);   // every bias (2 KB)
     const int lane = threadIdx.x & 63, l32 = lane & 31, h = lane >> 5;
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int n = blockIdx.x;
     const char* prm = reinterpret_cast<const char*>(A.prm);
+    if (r0 >= A.H) return;   // workgroup-uniform (no band rows: nothing issued yet)
     // LDS-DMA of `kb` 1-KB pieces from the parameter image at `src` to LDS offset `dst`
     auto dma = [&](int src, int dst, int kb) {
         for (int i = wv; i < kb; i += CK_NW) ck_glds(prm + src + i * 1024 + lane * 16, lds0 + (unsigned)(dst + i * 1024));
     };
 
     // prologue: conv1's weights into the second weight buffer, conv2's into T (free until the
-    // first Residual conv writes it), the biases, the first 3x3 half
+    // first Residual conv writes it) and the first 3x3 half into the first buffer; a region too
+    // small for conv2's 16 KB takes them in the first buffer, the 3x3 half then follows phase A
+    const bool w2_in_t = RPX * CK_PX >= 16 * 1024;   // uniform
     dma(L.w1, wb_off + WBH, 16);
-    dma(L.w2, (int)(TT - sm), 16);
+    dma(L.w2, w2_in_t ? (int)(TT - sm) : wb_off, 16);
+    if (w2_in_t) dma(L.wr, wb_off, 18);
     dma(L.b1, (int)((const char*)BI - sm), (L.total - L.b1) / 1024);
-    dma(L.wr, wb_off, 18);
     if (threadIdx.x < 8) *reinterpret_cast<uint4*>(ZR + threadIdx.x * 16) = make_uint4(0, 0, 0, 0);
-    // the wave's pixel tile: 32 consecutive pixels (clamped; only p < HW is written)
+    // the wave's pixel tile: 32 consecutive region pixels (clamped; only p < NRP is written)
     const int p = wv * 32 + l32;
-    const bool own = wv * 32 < HW;                   // wave-uniform: the wave has a tile
-    const bool pv = p < HW;
-    const int pc = pv ? p : HW - 1;
-    const int py = pc / A.W, px = pc - py * A.W;
-    const T* xp = reinterpret_cast<const T*>(A.x) + ((long long)n * HW + pc) * A.ldx + 8 * h;
+    const bool own = wv * 32 < NRP;                  // wave-uniform: the wave has a tile
+    const bool pv = p < NRP;
+    const int pc = pv ? p : NRP - 1;
+    const int py = ra0 + pc / A.W, px = pc - (py - ra0) * A.W;   // image row / column
+    // rows of the wave's tile (wave-uniform): a phase runs the tile iff it meets the phase's rows
+    const int ty0 = ra0 + (wv * 32) / A.W, ty1 = ra0 + (min(wv * 32 + 31, NRP - 1)) / A.W;
+    auto live = [&](int lo, int hi) { return own && ty1 >= lo && ty0 < hi; };
+    const T* xp = reinterpret_cast<const T*>(A.x) + (((long long)n * A.H + py) * A.W + px) * A.ldx + 8 * h;
     uint4 xb[8];
 #pragma unroll
     for (int kb = 0; kb < 8; ++kb) xb[kb] = *reinterpret_cast<const uint4*>(xp + 16 * kb);
@@ -155,7 +179,7 @@ __global__ __launch_bounds__(CK_THREADS, 1) void c3k_fused(const C3kArgs A) {
     uint4 bf[8];
     f32x16 acc;
     if (own) {
-        const char* w2 = TT;
+        const char* w2 = w2_in_t ? TT : WB;
         const float* b2 = BI + (L.b2 - L.b1) / 4;
 #pragma unroll
         for (int t = 0; t < 2; ++t) {
@@ -191,6 +215,10 @@ __global__ __launch_bounds__(CK_THREADS, 1) void c3k_fused(const C3kArgs A) {
             }
         }
     }
+    if (!w2_in_t) {
+        ck_barrier();   // conv2's weights read: the first 3x3 half may land in the first buffer
+        dma(L.wr, wb_off, 18);
+    }
 
     // 3x3 taps of the wave's pixel: pixel byte offset within C1 / T with the chunk swizzle in
     // its low bits (-128: outside the image, read from the zero block)
@@ -198,8 +226,10 @@ __global__ __launch_bounds__(CK_THREADS, 1) void c3k_fused(const C3kArgs A) {
 #pragma unroll
     for (int t = 0; t < 9; ++t) {
         const int yy = py + t / 3 - 1, xx = px + t % 3 - 1;
-        const bool in = (unsigned)yy < (unsigned)A.H && (unsigned)xx < (unsigned)A.W;
-        const int q = yy * A.W + xx;
+        // outside the image: the zero block; outside the region (only taps of pixels whose
+        // outputs no later phase reads): the zero block too
+        const bool in = yy >= ra0 && yy < ra1 && (unsigned)xx < (unsigned)A.W;
+        const int q = (yy - ra0) * A.W + xx;
         tq[t] = in ? (q * CK_PX) | ((q >> 1) & 7) : -CK_PX;
     }
     const int zr_off = (int)(ZR - sm);
@@ -217,7 +247,9 @@ __global__ __launch_bounds__(CK_THREADS, 1) void c3k_fused(const C3kArgs A) {
         ck_barrier();   // ... and everyone's; the other buffer and the previous phase are done
         if (hs + 1 < 16) dma(L.wr + (hs + 1) * WBH, wb_off + ((hs + 1) & 1) * WBH, 18);
         else dma(L.w3, wb_off, 16);
-        if (!own) continue;
+        // rows this conv must produce: the band + (3 - cv) halo rows (what conv cv + 1 reads)
+        const int lo = max(0, r0 - (3 - cv)), hi = min(A.H, r1 + (3 - cv));
+        if (!live(lo, hi)) continue;
         const int src_off = (int)(src - sm);
         int tb[9];
 #pragma unroll
@@ -239,7 +271,7 @@ __global__ __launch_bounds__(CK_THREADS, 1) void c3k_fused(const C3kArgs A) {
         if (half == 0) continue;
         unsigned w[8];
         ck_act<T>(acc, BI + (L.br - L.b1) / 4 + 64 * cv + 32 * t + 16 * h, w);
-        if (pv) {
+        if (pv && py >= lo && py < hi) {
             const int o0 = ck_off(p, 4 * t + 2 * h), o1 = ck_off(p, 4 * t + 2 * h + 1);
             if (cv & 1) {   // conv2 of a Residual: + its input (C1), rounded again (nn.py:49)
                 const uint4 r0 = *reinterpret_cast<const uint4*>(C1 + o0);
@@ -258,8 +290,9 @@ __global__ __launch_bounds__(CK_THREADS, 1) void c3k_fused(const C3kArgs A) {
     ck_barrier();
     dma(L.w3 + 16 * 1024, wb_off + WBH, 16);
     const float* b3 = BI + (L.b3 - L.b1) / 4;
-    T* y = reinterpret_cast<T*>(A.y) + ((long long)n * HW + pc) * A.ldy;
-    if (own) {
+    T* y = reinterpret_cast<T*>(A.y) + (((long long)n * A.H + py) * A.W + px) * A.ldy;
+    const bool fl = live(r0, r1);
+    if (fl) {
 #pragma unroll
         for (int kb = 0; kb < 4; ++kb) bf[kb] = *reinterpret_cast<const uint4*>(C1 + ck_off(pc, 2 * kb + h));
     }
@@ -269,7 +302,7 @@ __global__ __launch_bounds__(CK_THREADS, 1) void c3k_fused(const C3kArgs A) {
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             ck_barrier();
         }
-        if (!own) continue;
+        if (!fl) continue;
         const char* w3 = WB + (t >> 1) * WBH + (t & 1) * 8 * 1024;
 #pragma unroll
         for (int e = 0; e < 16; ++e) acc[e] = 0.f;
@@ -278,7 +311,7 @@ __global__ __launch_bounds__(CK_THREADS, 1) void c3k_fused(const C3kArgs A) {
             acc = KMfma<T>::step(*reinterpret_cast<const uint4*>(w3 + (kb * 64 + lane) * 16), bf[kb], acc);
         unsigned w[8];
         ck_act<T>(acc, b3 + 32 * t + 16 * h, w);
-        if (pv) {
+        if (pv && py >= r0 && py < r1) {
             uint4* d = reinterpret_cast<uint4*>(y + 32 * t + 16 * h);
             d[0] = make_uint4(w[0], w[1], w[2], w[3]);
             d[1] = make_uint4(w[4], w[5], w[6], w[7]);
@@ -286,17 +319,26 @@ __global__ __launch_bounds__(CK_THREADS, 1) void c3k_fused(const C3kArgs A) {
     }
 }
 
+// LDS bytes for region images of rpx pixels: C1 + T, two 18 KB weight halves (also conv1 /
+// conv2 / conv3's 32 KB), the zero block, the biases
+static long long ck_lds_px(long long rpx) {
+    return 2 * rpx * CK_PX + 36 * 1024 + 128 + (ck_layout().total - ck_layout().b1);
+}
+
 template <typename T>
-int launch_c3k_t(const C3kArgs& a, hipStream_t s) {
-    const int lds = c3k_lds(a.H, a.W);
-    if (lds == 0 || a.B < 1 || a.ldx % 8 || a.ldy % 8) return (int)hipErrorInvalidValue;
+int launch_c3k_t(const C3kArgs& a0, hipStream_t s) {
+    C3kArgs a = a0;
+    a.bands = c3k_bands(a.B, a.H, a.W);
+    const long long lds = ck_lds_px(ck_region_px(a.H, a.W, a.bands));
+    if (c3k_lds(a.H, a.W) == 0 || lds > 160 * 1024 || a.B < 1 || a.ldx % 8 || a.ldy % 8)
+        return (int)hipErrorInvalidValue;
     static bool attr = false;
     if (!attr) {
         (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&c3k_fused<T>), hipFuncAttributeMaxDynamicSharedMemorySize,
                                   160 * 1024);
         attr = true;
     }
-    hipLaunchKernelGGL((c3k_fused<T>), dim3((unsigned)a.B), dim3(CK_THREADS), lds, s, a);
+    hipLaunchKernelGGL((c3k_fused<T>), dim3((unsigned)(a.B * a.bands)), dim3(CK_THREADS), (int)lds, s, a);
     return (int)hipGetLastError();
 }
 
@@ -313,10 +355,19 @@ void c3k_offsets(int (&off)[9]) {
 int c3k_lds(int H, int W) {
     const long long hw = (long long)H * W;
     if (H < 1 || W < 1 || hw > 32 * CK_NW) return 0;
-    // C1 + T (T also holds conv3's 32 KB of weights in the last phase), two 18 KB weight
-    // halves, the zero block, the biases
-    const long long b = hw * CK_PX + std::max(hw * CK_PX, 32LL * 1024) + 36 * 1024 + 128 + (ck_layout().total - ck_layout().b1);
+    const long long b = ck_lds_px(hw);
     return b <= 160 * 1024 ? (int)b : 0;
+}
+
+int c3k_region_px(int H, int W, int bands) { return ck_region_px(H, W, bands); }
+
+int c3k_bands(int B, int H, int W) {
+    // enough workgroups for the chip (>= 128) with bands of >= 4 rows; YH_C3K_BANDS overrides
+    int r = std::max(1, std::min((128 + B - 1) / B, H / 4));
+    if (const char* e = getenv("YH_C3K_BANDS")) r = std::max(1, std::min(atoi(e), H));
+    while (r > 1 && ck_region_px(H, W, r) > 32 * CK_NW) --r;   // never: a band region <= the image
+    (void)W;
+    return r;
 }
 
 int launch_c3k(int dtype, const C3kArgs& a, hipStream_t s) {

@@ -176,10 +176,13 @@ struct C3kArgs {
     void* y; int ldy;                // block output view (c channels)
     int B, H, W;
     const void* prm;                 // packed parameters (c3k_offsets)
+    int bands;                       // row bands per image (set by launch_c3k: c3k_bands)
 };
 int c3k_prm_bytes();
 void c3k_offsets(int (&off)[9]);     // w1, w2, residual convs, w3, b1, b2, residual biases, b3, total
 int c3k_lds(int H, int W);           // 0: the image does not fit
+int c3k_bands(int B, int H, int W);  // row bands per image (one workgroup each)
+int c3k_region_px(int H, int W, int bands);   // LDS pixels of a band's region (band + 4-row halo)
 int launch_c3k(int dtype, const C3kArgs& a, hipStream_t s);
 
 // Box tail of the detect head, one launch for all levels: the last box conv (Conv2d 1x1

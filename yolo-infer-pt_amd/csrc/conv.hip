@@ -786,14 +786,24 @@ __global__ __launch_bounds__(S2_NT) void stem_fused(const Stem2Args p) {
                 const int q = (2 * r + kh) * S2_SC + 2 * l32 + kw;
                 acc = s2_mfma<T>(af[s], sout[q * PS + 2 * cb + h], acc);
             }
-            const int ho = ho0 + r, wo = wo0 + l32;
-            if (ho < p.Ho && wo < p.Wo) {
-                unsigned w[8];
+            // the row's 32 pixels x 32 couts through the wave's 2 KB of the (dead) input window:
+            // 4 lanes per pixel store 64 contiguous bytes (one pixel per lane would write 2 x 16 B
+            // of each of 32 pixels per instruction; conv_mx.hip co_stage)
+            unsigned w[8];
 #pragma unroll
-                for (int e = 0; e < 16; e += 2) w[e >> 1] = s2_pack2<T>(silu<T>(acc[e] + b2[e]), silu<T>(acc[e + 1] + b2[e + 1]));
-                uint4* d = reinterpret_cast<uint4*>(out + (((long long)n * p.Ho + ho) * p.Wo + wo) * p.ldo + co);
-                d[0] = make_uint4(w[0], w[1], w[2], w[3]);
-                d[1] = make_uint4(w[4], w[5], w[6], w[7]);
+            for (int e = 0; e < 16; e += 2) w[e >> 1] = s2_pack2<T>(silu<T>(acc[e] + b2[e]), silu<T>(acc[e + 1] + b2[e + 1]));
+            char* E = reinterpret_cast<char*>(&patch[0][0]) + wave * 2048;
+            const int sw = (l32 >> 1) & 3;
+            *reinterpret_cast<uint4*>(E + (l32 * 4 + ((2 * h) ^ sw)) * 16) = make_uint4(w[0], w[1], w[2], w[3]);
+            *reinterpret_cast<uint4*>(E + (l32 * 4 + ((2 * h + 1) ^ sw)) * 16) = make_uint4(w[4], w[5], w[6], w[7]);
+            const int ho = ho0 + r;
+#pragma unroll
+            for (int k2 = 0; k2 < 2; ++k2) {
+                const int pp = k2 * 16 + (lane >> 2), qq = lane & 3;
+                const uint4 v = *reinterpret_cast<const uint4*>(E + (pp * 4 + (qq ^ ((pp >> 1) & 3))) * 16);
+                const int wo = wo0 + pp;
+                if (ho < p.Ho && wo < p.Wo)
+                    *reinterpret_cast<uint4*>(out + (((long long)n * p.Ho + ho) * p.Wo + wo) * p.ldo + 32 * a2 + 8 * qq) = v;
             }
         }
     }

@@ -121,6 +121,7 @@ struct MxShape {
 struct RwGeo {
     int nw, cpp, nks, tpx, th, pr, pc, nbi, nbr, slot;   // nbr: residual DMA instructions (res)
     int red;                                             // LDS bytes of the K-chunk partials
+    int epi;                                             // LDS bytes of the epilogue staging tiles
 };
 RwGeo rw_geo(int S, int cin, int ncg, int npg, int mb, int tw, bool res, int nkc);
 // K chunks of a layer's canonical order (1: the plain walk). Shape-dependent (kernel,

@@ -177,6 +177,91 @@ __device__ __forceinline__ void mx_epi(const f32x16 (&acc)[NA], const float* bv,
     }
 }
 
+// Coalesced epilogue (tools/micro/access_rate: 16-B stores with one pixel per lane, 32 B of
+// each of 32 lines per wave-instruction, write 2.3 TB/s against 4.6 TB/s for whole-line
+// instructions, MALL-resident, 3.6 against 5.8-6.1 TB/s to HBM). The wave's 32-pixel x BN-cout
+// B tile goes through LDS: each lane writes its pixel's 16*NA couts (bias, activation, one
+// rounding done), then reads back LPP = 4*NA lanes per pixel, so every store instruction writes
+// 64 / LPP whole pixel rows of BN*2 bytes; the residual is read in the same shape and added after
+// the rounding, as in mx_epi (bit-identical). Row slots are XOR-swizzled by the pixel: the
+// ds_write_b128 groups of 8 lanes (8 pixels, one chunk) and the ds_read_b128 groups hit
+// distinct banks.
+template <int NA>
+__device__ __forceinline__ int co_swz(int p) { return NA == 1 ? ((p >> 1) & 3) : (p & 7); }
+
+template <typename T, int NA, bool SILU>
+__device__ __forceinline__ void co_stage(const f32x16 (&acc)[NA], const float* bv, char* E, int l32, int h) {
+    constexpr int LPP = 4 * NA;
+#pragma unroll
+    for (int c8 = 0; c8 < 2 * NA; ++c8) {
+        unsigned w[4];
+#pragma unroll
+        for (int e = 0; e < 8; e += 2) {
+            const int i0 = c8 * 8 + e, i1 = i0 + 1;
+            float x0 = acc[i0 >> 4][i0 & 15] + bv[i0];
+            float x1 = acc[i1 >> 4][i1 & 15] + bv[i1];
+            if constexpr (SILU) {
+                x0 = silu<T>(x0);
+                x1 = silu<T>(x1);
+            }
+            w[e >> 1] = pack2<T>(x0, x1);
+        }
+        const int q = 2 * NA * h + c8;
+        *reinterpret_cast<uint4*>(E + (l32 * LPP + (q ^ co_swz<NA>(l32))) * 16) = make_uint4(w[0], w[1], w[2], w[3]);
+    }
+}
+
+template <typename T>
+__device__ __forceinline__ uint4 co_addres(uint4 v, const T* rp) {
+    const uint4 r = *reinterpret_cast<const uint4*>(rp);
+    const unsigned vv[4] = {v.x, v.y, v.z, v.w}, rr[4] = {r.x, r.y, r.z, r.w};
+    unsigned w[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) w[q] = pack2<T>(lo16<T>(vv[q]) + lo16<T>(rr[q]), hi16<T>(vv[q]) + hi16<T>(rr[q]));
+    return make_uint4(w[0], w[1], w[2], w[3]);
+}
+
+// One 32-pixel B tile through the wave's staging image E (64 * 32 * NA bytes): stage, read back
+// 4*NA lanes per pixel, add the residual, store. bt = B tile index within the task, c0 = first
+// cout of the wave's BN-wide block; (n, hh0, ww0) = the task's origin (KS 1: flat pixel ww0).
+template <typename T, int NA, int KS>
+__device__ __forceinline__ void co_tile(const f32x16 (&aj)[NA], const float* bv, bool silu_act, char* E, int lane,
+                                        const MxArgs& p, int n, int hh0, int ww0, int bt, int c0, const T* res, T* out,
+                                        bool no_store) {
+    constexpr int LPP = 4 * NA, PPI = 64 / LPP;
+    const int l32 = lane & 31, h = lane >> 5;
+    if (silu_act) co_stage<T, NA, true>(aj, bv, E, l32, h);
+    else co_stage<T, NA, false>(aj, bv, E, l32, h);
+    const int qr = lane % LPP, pr0 = lane / LPP;
+    const int cq = c0 + 8 * qr;
+    const bool cq_ok = cq < p.cout;
+#pragma unroll
+    for (int k = 0; k < 2 * NA; ++k) {
+        const int pp = k * PPI + pr0;
+        const uint4 v = *reinterpret_cast<const uint4*>(E + (pp * LPP + (qr ^ co_swz<NA>(pp))) * 16);
+        long long m;
+        bool ok;
+        if constexpr (KS == 3) {
+            const int bc = 1 << p.bc_log2, btw = p.TW >> p.bc_log2;
+            const int btr = bt / btw, btc = bt - btr * btw;
+            const int ho = hh0 + btr * (32 >> p.bc_log2) + (pp >> p.bc_log2);
+            const int wo = ww0 + btc * bc + (pp & (bc - 1));
+            ok = ho < p.Ho && wo < p.Wo;
+            m = ((long long)n * p.Ho + ho) * p.Wo + wo;
+        } else {
+            const int mm = ww0 + bt * 32 + pp;
+            ok = mm < p.M;
+            m = mm;
+        }
+        ok = ok && cq_ok;
+        if (!ok) m = 0;
+        const int cc = ok ? cq : 0;
+        uint4 o = v;
+        if (res) o = co_addres<T>(v, res + m * p.ldr + cc);
+        if (ok && !no_store) *reinterpret_cast<uint4*>(out + m * p.ldo + cc) = o;
+    }
+}
+
 template <typename T, int KS, int S, int NA, int MB, int WN, int WM, int NCB>
 __global__ __launch_bounds__(64 * WN * WM, 2) void conv_mx(const MxArgs p) {
     constexpr int NW = WN * WM, NT = 64 * NW;
@@ -401,7 +486,11 @@ __global__ __launch_bounds__(64 * WN * WM, 2) void conv_mx(const MxArgs p) {
     // the stores (and the uniform residual switch): every load it issues is consumed on
     // every path, so no load is left in flight across the loop back-edge (hipcc would
     // otherwise wait for it in the next compute phase, draining the prefetch DMA).
-    auto epilogue = [&](int tk) {
+    // coalesced epilogue (co_tile): after a barrier every wave has multiplied the last stage, so
+    // that stage's buffer (weights + patch) is free until the next iteration issues into it,
+    // which is after the barrier that closes this one
+    const bool co_fits = NW * 2048 * NA <= stage_ch * 16;   // uniform
+    auto epilogue = [&](int tk, int g) {
         int n, hh0, ww0, sl;
         decompose(tk, n, hh0, ww0, sl);
         const int co = sl * BN + co_lane;
@@ -415,6 +504,19 @@ __global__ __launch_bounds__(64 * WN * WM, 2) void conv_mx(const MxArgs p) {
         }
         const T* res = reinterpret_cast<const T*>(p.res);
         T* out = reinterpret_cast<T*>(p.out);
+        if (co_fits) {
+            mx_barrier();
+            char* E = reinterpret_cast<char*>(sm4) + ((g & 1) * stage_ch) * 16 + wv * 2048 * NA;
+#pragma unroll
+            for (int j = 0; j < MB; ++j) {
+                f32x16 aj[NA];
+#pragma unroll
+                for (int a = 0; a < NA; ++a) aj[a] = acc[a][j];
+                co_tile<T, NA, KS>(aj, bv, p.act == ACT_SILU, E, lane, p, n, hh0, ww0, wm * MB + j, sl * BN + wn * NA * 32,
+                                   res, out, false);
+            }
+            return;
+        }
 #pragma unroll
         for (int j = 0; j < MB; ++j) {
             long long m;
@@ -465,7 +567,7 @@ __global__ __launch_bounds__(64 * WN * WM, 2) void conv_mx(const MxArgs p) {
                     for (int e = 0; e < 16; ++e) acc[a][j][e] = 0.f;
         }
         if (!(MX_DBG(4))) compute((g & 1) * stage_ch);
-        if (st == p.nst - 1 && !(MX_DBG(8))) epilogue(t_lo + g / p.nst);
+        if (st == p.nst - 1 && !(MX_DBG(8))) epilogue(t_lo + g / p.nst, g);
         mx_barrier();
     }
     if (MX_TRACE && threadIdx.x == 0) {
@@ -688,7 +790,10 @@ __global__ __launch_bounds__(64 * NW, 2) void conv_mxr(const MxArgs p) {
 
     const int co = sl * BN + 16 * NA * h;
     const bool co_ok = co < p.cout;
-    auto epilogue = [&](int tk) {
+    // coalesced epilogue through the patch buffer the last stage just freed (NBUF 2: the next
+    // stage's DMA goes to the other buffer; the one after it is issued only after these reads)
+    constexpr bool CO = NBUF == 2 && NBI * 1024 >= 2048 * NA;
+    auto epilogue = [&](int tk, int g) {
         int n, hh0, ww0;
         tile_pos(tk, n, hh0, ww0);
         float bv[16 * NA];
@@ -700,6 +805,18 @@ __global__ __launch_bounds__(64 * NW, 2) void conv_mxr(const MxArgs p) {
         }
         const T* res = reinterpret_cast<const T*>(p.res);
         T* out = reinterpret_cast<T*>(p.out);
+        if constexpr (CO) {
+            char* E = reinterpret_cast<char*>(sm4) + (pbuf + (g & 1) * BUFCH) * 16;
+#pragma unroll
+            for (int j = 0; j < MB; ++j) {
+                f32x16 aj[NA];
+#pragma unroll
+                for (int a = 0; a < NA; ++a) aj[a] = acc[a][j];
+                co_tile<T, NA, KS>(aj, bv, p.act == ACT_SILU && !(MX_DBG(16)), E, lane, p, n, hh0, ww0, j, sl * BN, res,
+                                   out, MX_DBG(8));
+            }
+            return;
+        }
 #pragma unroll
         for (int j = 0; j < MB; ++j) {
             long long m;
@@ -754,7 +871,7 @@ __global__ __launch_bounds__(64 * NW, 2) void conv_mxr(const MxArgs p) {
         if (!(MX_DBG(4))) compute(g);
         // single buffer: the next stage's DMA may only start once this stage's reads are done
         if (NBUF == 1 && more) issue(g + 1);
-        if (st == p.nst - 1 && !(MX_DBG(8))) epilogue(t_lo + g / p.nst);
+        if (st == p.nst - 1 && !(MX_DBG(8) && !CO)) epilogue(t_lo + g / p.nst, g);
     }
 }
 

@@ -50,6 +50,7 @@ RwGeo rw_geo(int S, int cin, int ncg, int npg, int mb, int tw, bool res, int nkc
     g.nbr = res ? (g.tpx * ncg * 4 + 64 * g.nw - 1) / (64 * g.nw) : 0;
     g.slot = (g.nbi + g.nbr) * g.nw * 1024;
     g.red = (nkc - 1) * ncg * npg * mb * 4096;
+    g.epi = ncg * npg * 2048;   // coalesced epilogue: one 32-pixel x 32-cout staging tile per storing wave
     return g;
 }
 
@@ -141,6 +142,7 @@ __global__ __launch_bounds__(64 * NCG * NKC * NPG, NCG * NKC * NPG >= 8 ? 2 : 1)
     constexpr int RSH = NCG == 1 ? 2 : NCG == 2 ? 1 : 0;   // residual image swizzle: chunk ^ (px >> RSH)
     constexpr int NBR = RES ? (TPX * RCH + 64 * NW - 1) / (64 * NW) : 0;
     constexpr int SLOT = (NBI + NBR) * NW * 1024;
+    constexpr int RED = (NKC - 1) * NCG * NPG * MB * 4096;   // K-chunk partials (rw_geo's red)
     static_assert(TPX % TW == 0 && (CPP & (CPP - 1)) == 0 && NS >= 2 && NKT % NKC == 0, "rw geometry");
     // VMEM ops a wave issues after its DMAs of tile it, still uncounted at the wait of
     // iteration it: the epilogues (2 stores per B tile; only the chunk-0 waves store) of the
@@ -278,7 +280,6 @@ __global__ __launch_bounds__(64 * NCG * NKC * NPG, NCG * NKC * NPG >= 8 ? 2 : 1)
 
     const __amdgpu_buffer_rsrc_t ro = rw_rsrc(p.out);
     const bool silu_act = p.act == ACT_SILU;
-    const unsigned co_b = (unsigned)(co0 + 16 * h) * 2u;
 
     rw_f32x16 acc[MB];
     for (int it = 0; it < n_it; ++it) {
@@ -342,40 +343,54 @@ __global__ __launch_bounds__(64 * NCG * NKC * NPG, NCG * NKC * NPG >= 8 ? 2 : 1)
             }
         }
         // ---- epilogue (chunk-0 waves): bias, activation, one rounding (the conv output), the
-        //      residual added in fp32 and rounded again (nets/nn.py:49); 2 x 16-B stores per
-        //      lane and B tile
+        //      residual added in fp32 and rounded again (nets/nn.py:49). The wave's 32 pixels x
+        //      32 couts go through its private LDS staging tile (lane (r32, h) writes its 16
+        //      couts, 4 lanes per pixel read 64 contiguous bytes back: every store instruction
+        //      writes 16 pixels x 64 B instead of 32 pixels x 2 x 16 B; conv_mx.hip co_stage)
         if (kc == 0) {
             int n, ty0, tx0;
             tile_pos(it, n, ty0, tx0);
+            char* E = reinterpret_cast<char*>(sm4) + NS * SLOT + RED + (pg * NCG + cg) * 2048;
+            const int qr = lane & 3, pr0 = lane >> 2;
 #pragma unroll
             for (int j = 0; j < MB; ++j) {
-                const int oy = ty0 + pty[j], ox = tx0 + ptx[j];
-                const bool ok = oy < p.Ho && ox < p.Wo;
-                const long long m = ((long long)n * p.Ho + oy) * p.Wo + ox;
-                const unsigned oo = ok ? (unsigned)(m * p.ldo * 2) + co_b : RW_OOB;
-                unsigned w[8];
 #pragma unroll
-                for (int e = 0; e < 16; e += 2) {
-                    float x0 = acc[j][e] + bv[e], x1 = acc[j][e + 1] + bv[e + 1];
-                    if (silu_act) {
-                        x0 = silu<T>(x0);
-                        x1 = silu<T>(x1);
+                for (int c = 0; c < 2; ++c) {
+                    unsigned w[4];
+#pragma unroll
+                    for (int e = 0; e < 8; e += 2) {
+                        float x0 = acc[j][8 * c + e] + bv[8 * c + e], x1 = acc[j][8 * c + e + 1] + bv[8 * c + e + 1];
+                        if (silu_act) {
+                            x0 = silu<T>(x0);
+                            x1 = silu<T>(x1);
+                        }
+                        w[e >> 1] = rw_pack2<T>(x0, x1);
                     }
-                    w[e >> 1] = rw_pack2<T>(x0, x1);
+                    const int q = 2 * h + c;
+                    *reinterpret_cast<uint4*>(E + (r32 * 4 + (q ^ ((r32 >> 1) & 3))) * 16) = make_uint4(w[0], w[1], w[2], w[3]);
                 }
-                if constexpr (RES) {
-                    const int px = (pg * MB + j) * 32 + r32, f = (px >> RSH) & (RCH - 1);
-                    const char* rb = reinterpret_cast<const char*>(sm4) + (it % NS) * SLOT + NBI * NW * 1024 + px * RCH * 16;
-                    const uint4 r0 = *reinterpret_cast<const uint4*>(rb + ((cg * 4 + 2 * h) ^ f) * 16);
-                    const uint4 r1 = *reinterpret_cast<const uint4*>(rb + ((cg * 4 + 2 * h + 1) ^ f) * 16);
-                    const unsigned rv[8] = {r0.x, r0.y, r0.z, r0.w, r1.x, r1.y, r1.z, r1.w};
 #pragma unroll
-                    for (int q = 0; q < 8; ++q)
-                        w[q] = rw_pack2<T>(rw_lo<T>(w[q]) + rw_lo<T>(rv[q]), rw_hi<T>(w[q]) + rw_hi<T>(rv[q]));
+                for (int k = 0; k < 2; ++k) {
+                    const int pp = k * 16 + pr0;
+                    const uint4 v = *reinterpret_cast<const uint4*>(E + (pp * 4 + (qr ^ ((pp >> 1) & 3))) * 16);
+                    unsigned w[4] = {v.x, v.y, v.z, v.w};
+                    const int px = (pg * MB + j) * 32 + pp;
+                    const int oy = ty0 + px / TW, ox = tx0 + px % TW;
+                    const bool ok = oy < p.Ho && ox < p.Wo;
+                    const long long m = ((long long)n * p.Ho + oy) * p.Wo + ox;
+                    if constexpr (RES) {
+                        const int f = (px >> RSH) & (RCH - 1);
+                        const char* rb = reinterpret_cast<const char*>(sm4) + (it % NS) * SLOT + NBI * NW * 1024 + px * RCH * 16;
+                        const uint4 r = *reinterpret_cast<const uint4*>(rb + ((cg * 4 + qr) ^ f) * 16);
+                        const unsigned rv[4] = {r.x, r.y, r.z, r.w};
+#pragma unroll
+                        for (int q = 0; q < 4; ++q)
+                            w[q] = rw_pack2<T>(rw_lo<T>(w[q]) + rw_lo<T>(rv[q]), rw_hi<T>(w[q]) + rw_hi<T>(rv[q]));
+                    }
+                    const unsigned oo = ok ? (unsigned)(m * p.ldo * 2) + (unsigned)(co0 + 8 * qr) * 2u : RW_OOB;
+                    const unsigned od = RW_DBG(8) ? RW_OOB : oo;
+                    __builtin_amdgcn_raw_buffer_store_b128(rw_u32x4{w[0], w[1], w[2], w[3]}, ro, od, 0, 0);
                 }
-                const unsigned od = RW_DBG(8) ? RW_OOB : oo;
-                __builtin_amdgcn_raw_buffer_store_b128(rw_u32x4{w[0], w[1], w[2], w[3]}, ro, od, 0, 0);
-                __builtin_amdgcn_raw_buffer_store_b128(rw_u32x4{w[4], w[5], w[6], w[7]}, ro, od + 16u, 0, 0);
             }
         }
     }
@@ -452,7 +467,7 @@ MxPlan mx_plan_w(const MxShape& sh, const MxConfig& c, int num_cus) {
     pl.ntasks = sh.B * pl.ntw * pl.nth;
     pl.bbytes = g.slot;
     pl.abytes = 0;
-    pl.lds = c.nbuf * g.slot + g.red;
+    pl.lds = c.nbuf * g.slot + g.red + g.epi;
     if (pl.lds > 160 * 1024 || g.nw > 16) return pl;
     pl.wstage = pl.nslices * ncg * g.nks * 1024;   // packed weight bytes
     int best = 1 << 30, bsh = 0, bmr = 0;
@@ -557,7 +572,7 @@ namespace {
 template <typename T, int S, int CIN, int NCG, int NPG, int MB, int TW, int NS, bool RES, int NKC>
 int launch_rw_t(const MxPlan& pl, const MxArgs& a, hipStream_t s) {
     const RwGeo g = rw_geo(S, CIN, NCG, NPG, MB, TW, RES, NKC);
-    if (g.nbi != pl.nbi || NS * g.slot + g.red != pl.lds || RES != (a.res != nullptr)) return (int)hipErrorInvalidValue;
+    if (g.nbi != pl.nbi || NS * g.slot + g.red + g.epi != pl.lds || RES != (a.res != nullptr)) return (int)hipErrorInvalidValue;
     static bool attr = false;
     auto k = &conv_rw<T, S, CIN, NCG, NPG, MB, TW, NS, RES, NKC>;
     if (!attr) {
