@@ -31,6 +31,11 @@
 #include <algorithm>
 #include <cstring>
 
+#ifndef RW_PF
+#define RW_PF 1   // B-fragment prefetch distance of the MFMA loop, in k-steps
+#endif
+
+
 namespace yh {
 
 typedef __attribute__((ext_vector_type(16))) float rw_f32x16;
@@ -50,7 +55,8 @@ RwGeo rw_geo(int S, int cin, int ncg, int npg, int mb, int tw, bool res, int nkc
     g.nbr = res ? (g.tpx * ncg * 4 + 64 * g.nw - 1) / (64 * g.nw) : 0;
     g.slot = (g.nbi + g.nbr) * g.nw * 1024;
     g.red = (nkc - 1) * ncg * npg * mb * 4096;
-    g.epi = ncg * npg * 2048;   // coalesced epilogue: one 32-pixel x 32-cout staging tile per storing wave
+    // coalesced epilogue: one 32-pixel x 32-cout staging tile per storing wave, + the slice's bias
+    g.epi = ncg * npg * 2048 + ncg * 128;
     return g;
 }
 
@@ -252,27 +258,51 @@ __global__ __launch_bounds__(64 * NCG * NKC * NPG, NCG * NKC * NPG >= 8 ? 2 : 1)
         }
     };
 
-    // ---- prologue: the first NS-1 tiles' patches in flight, then the weights and bias
-    for (int k = 0; k < NS - 1; ++k) issue(k, k);
+    // ---- prologue: the weights and bias, and the first NS-1 tiles' patches in flight.
+    //      With several pixel groups (NPG > 1) NPG waves need each cout group's image: the
+    //      workgroup's images (NCG x NKT KB) come by LDS-DMA once into the (still idle) slot
+    //      ring and every wave reads its fragments from there, instead of NPG reads of each
+    //      image from L2 (r04 micro bench, box.0.0 shape: a 5 us setup, 75 MB of L2 reads per
+    //      launch against 37 MB of patches); the first patches are issued after that.
+    constexpr bool WLDS = NPG > 1 && NCG * NKT * 1024 <= NS * SLOT;
     const int co0 = (sl * NCG + cg) * 32;
     uint4 wf[NKS];
-    {
+    if constexpr (WLDS) {
+        // the images go to the END of the ring: the first tiles whose slots lie below them are
+        // issued before the images, the others once every wave holds its fragments
+        constexpr int NQ = NCG * NKT;
+        constexpr int WOFF = NS * SLOT - NQ * 1024;
+        constexpr int EARLY = WOFF / SLOT < NS - 1 ? WOFF / SLOT : NS - 1;
+        for (int k = 0; k < EARLY; ++k) issue(k, k);
+        const char* wimg = p.w + (long long)(sl * NCG) * NKT * 1024;
+        // every workgroup starts at another 1 KB piece: the 256 workgroups do not all read the
+        // same lines at the same moment
+        const int rot = (int)(blockIdx.x % NQ);
+        for (int q0 = wv; q0 < NQ; q0 += NW) {
+            const int q = q0 + rot < NQ ? q0 + rot : q0 + rot - NQ;
+            rw_glds(wimg + ((long long)q * 64 + lane) * 16, lds0 + (unsigned)(WOFF + q * 1024));
+        }
+        rw_vmwait<0>();
+        rw_barrier();
+        const char* wl = reinterpret_cast<const char*>(sm4) + WOFF + ((cg * NKT + kc * NKS) * 64 + lane) * 16;
+#pragma unroll
+        for (int s = 0; s < NKS; ++s) wf[s] = *reinterpret_cast<const uint4*>(wl + s * 1024);
+        rw_barrier();   // every wave holds its fragments: the rest of the ring may be filled
+        for (int k = EARLY; k < NS - 1; ++k) issue(k, k);
+    } else {
+        for (int k = 0; k < NS - 1; ++k) issue(k, k);
         const char* wsrc = p.w + ((long long)(sl * NCG + cg) * NKT * 64 + kc * NKS * 64 + lane) * 16;
 #pragma unroll
         for (int s = 0; s < NKS; ++s) wf[s] = *reinterpret_cast<const uint4*>(wsrc + (long long)s * 1024);
     }
-    float bv[16];
-#pragma unroll
-    for (int e = 0; e < 16; e += 4) {
-        const float4 b4 = *reinterpret_cast<const float4*>(p.bias + co0 + 16 * h + e);
-        bv[e] = b4.x; bv[e + 1] = b4.y; bv[e + 2] = b4.z; bv[e + 3] = b4.w;
-    }
+    // the slice's bias in LDS (read per B tile in the epilogue: 16 VGPRs free for the fragment
+    // prefetch ring)
+    float* bias_l = reinterpret_cast<float*>(reinterpret_cast<char*>(sm4) + NS * SLOT + RED + NCG * NPG * 2048);
+    if ((int)threadIdx.x < NCG * 32) bias_l[threadIdx.x] = p.bias[(sl * NCG) * 32 + threadIdx.x];
     // the compiler waits for these loads HERE (not at their first use inside the loop,
     // where its vmcnt(0) would drain the patch ring every iteration)
 #pragma unroll
     for (int s = 0; s < NKS; ++s) asm volatile("" :: "v"(wf[s].x), "v"(wf[s].y), "v"(wf[s].z), "v"(wf[s].w));
-#pragma unroll
-    for (int e = 0; e < 16; ++e) asm volatile("" :: "v"(bv[e]));
     rw_vmwait<0>();
     rw_barrier();
     const unsigned long long t_setup = RW_TRACE ? __builtin_amdgcn_s_memrealtime() : 0ull;
@@ -282,11 +312,71 @@ __global__ __launch_bounds__(64 * NCG * NKC * NPG, NCG * NKC * NPG >= 8 ? 2 : 1)
     const bool silu_act = p.act == ACT_SILU;
 
     rw_f32x16 acc[MB];
+    // ---- epilogue (chunk-0 waves): bias, activation, one rounding (the conv output), the
+    //      residual added in fp32 and rounded again (nets/nn.py:49). The wave's 32 pixels x
+    //      32 couts go through its private LDS staging tile (lane (r32, h) writes its 16
+    //      couts, 4 lanes per pixel read 64 contiguous bytes back: every store instruction
+    //      writes 16 pixels x 64 B instead of 32 pixels x 2 x 16 B; conv_mx.hip co_stage)
+    auto epilogue = [&](int it) {
+        int n, ty0, tx0;
+        tile_pos(it, n, ty0, tx0);
+        char* E = reinterpret_cast<char*>(sm4) + NS * SLOT + RED + (pg * NCG + cg) * 2048;
+        const int qr = lane & 3, pr0 = lane >> 2;
+        float bv[16];
+#pragma unroll
+        for (int e = 0; e < 16; e += 4) {
+            const float4 b4 = *reinterpret_cast<const float4*>(bias_l + cg * 32 + 16 * h + e);
+            bv[e] = b4.x; bv[e + 1] = b4.y; bv[e + 2] = b4.z; bv[e + 3] = b4.w;
+        }
+#pragma unroll
+        for (int j = 0; j < MB; ++j) {
+#pragma unroll
+            for (int c = 0; c < 2; ++c) {
+                unsigned w[4];
+#pragma unroll
+                for (int e = 0; e < 8; e += 2) {
+                    float x0 = acc[j][8 * c + e] + bv[8 * c + e], x1 = acc[j][8 * c + e + 1] + bv[8 * c + e + 1];
+                    if (silu_act) {
+                        x0 = silu<T>(x0);
+                        x1 = silu<T>(x1);
+                    }
+                    w[e >> 1] = rw_pack2<T>(x0, x1);
+                }
+                const int q = 2 * h + c;
+                *reinterpret_cast<uint4*>(E + (r32 * 4 + (q ^ ((r32 >> 1) & 3))) * 16) = make_uint4(w[0], w[1], w[2], w[3]);
+            }
+#pragma unroll
+            for (int k = 0; k < 2; ++k) {
+                const int pp = k * 16 + pr0;
+                const uint4 v = *reinterpret_cast<const uint4*>(E + (pp * 4 + (qr ^ ((pp >> 1) & 3))) * 16);
+                unsigned w[4] = {v.x, v.y, v.z, v.w};
+                const int px = (pg * MB + j) * 32 + pp;
+                const int oy = ty0 + px / TW, ox = tx0 + px % TW;
+                const bool ok = oy < p.Ho && ox < p.Wo;
+                const long long m = ((long long)n * p.Ho + oy) * p.Wo + ox;
+                if constexpr (RES) {
+                    const int f = (px >> RSH) & (RCH - 1);
+                    const char* rb = reinterpret_cast<const char*>(sm4) + (it % NS) * SLOT + NBI * NW * 1024 + px * RCH * 16;
+                    const uint4 r = *reinterpret_cast<const uint4*>(rb + ((cg * 4 + qr) ^ f) * 16);
+                    const unsigned rv[4] = {r.x, r.y, r.z, r.w};
+#pragma unroll
+                    for (int q = 0; q < 4; ++q)
+                        w[q] = rw_pack2<T>(rw_lo<T>(w[q]) + rw_lo<T>(rv[q]), rw_hi<T>(w[q]) + rw_hi<T>(rv[q]));
+                }
+                const unsigned oo = ok ? (unsigned)(m * p.ldo * 2) + (unsigned)(co0 + 8 * qr) * 2u : RW_OOB;
+                const unsigned od = RW_DBG(8) ? RW_OOB : oo;
+                __builtin_amdgcn_raw_buffer_store_b128(rw_u32x4{w[0], w[1], w[2], w[3]}, ro, od, 0, 0);
+            }
+        }
+    };
+    unsigned long long t_wait = 0ull;   // diagnostic builds, dbg 64: time spent in the loop-top waits
     for (int it = 0; it < n_it; ++it) {
         if (it > 0) {
+            const unsigned long long tw0 = (RW_TRACE && RW_DBG(64)) ? __builtin_amdgcn_s_memrealtime() : 0ull;
             if (kc == 0) rw_vmwait<CNT0>();
             else rw_vmwait<CNT1>();
             rw_barrier();   // tile it complete in its slot; slot (it - 1) % NS read by every wave
+            if (RW_TRACE && RW_DBG(64)) t_wait += __builtin_amdgcn_s_memrealtime() - tw0;
             if (RW_TRACE && it == 1) t_first = __builtin_amdgcn_s_memrealtime();
         }
         issue(it + NS - 1, (it + NS - 1) % NS);
@@ -296,7 +386,10 @@ __global__ __launch_bounds__(64 * NCG * NKC * NPG, NCG * NKC * NPG >= 8 ? 2 : 1)
         {
             const char* Bp = reinterpret_cast<const char*>(sm4) + (it % NS) * SLOT;
             auto rd = [](const char* q) { return *reinterpret_cast<const uint4*>(__builtin_assume_aligned(q, 16)); };
-            uint4 bf[2][MB];
+            // B fragments read RW_PF k-steps ahead (a ring of RW_PF + 1): one ds_read_b128 feeds
+            // one 32-cycle MFMA, shorter than the read's latency
+            constexpr int PF = RW_PF, RING = RW_PF + 1;
+            uint4 bf[RING][MB];
             auto load = [&](int s, int buf) {
                 const int cb = s / 9, t = s - (s / 9) * 9;
 #pragma unroll
@@ -306,15 +399,16 @@ __global__ __launch_bounds__(64 * NCG * NKC * NPG, NCG * NKC * NPG >= 8 ? 2 : 1)
             for (int j = 0; j < MB; ++j)
 #pragma unroll
                 for (int e = 0; e < 16; ++e) acc[j][e] = 0.f;
-            load(0, 0);
-            __builtin_amdgcn_sched_group_barrier(0x100, MB, 0);
+#pragma unroll
+            for (int s = 0; s < PF && s < NKS; ++s) load(s, s % RING);
+            __builtin_amdgcn_sched_group_barrier(0x100, MB * (PF < NKS ? PF : NKS), 0);
 #pragma unroll
             for (int s = 0; s < NKS; ++s) {
-                if (s + 1 < NKS) load(s + 1, (s + 1) & 1);
+                if (s + PF < NKS) load(s + PF, (s + PF) % RING);
                 if (RW_DBG(4)) continue;
 #pragma unroll
-                for (int j = 0; j < MB; ++j) acc[j] = RwMfma<T>::step(wf[s], bf[s & 1][j], acc[j]);
-                if (s + 1 < NKS) __builtin_amdgcn_sched_group_barrier(0x100, MB, 0);
+                for (int j = 0; j < MB; ++j) acc[j] = RwMfma<T>::step(wf[s], bf[s % RING][j], acc[j]);
+                if (s + PF < NKS) __builtin_amdgcn_sched_group_barrier(0x100, MB, 0);
                 __builtin_amdgcn_sched_group_barrier(0x008, MB, 0);
             }
         }
@@ -342,61 +436,13 @@ __global__ __launch_bounds__(64 * NCG * NKC * NPG, NCG * NKC * NPG >= 8 ? 2 : 1)
                 }
             }
         }
-        // ---- epilogue (chunk-0 waves): bias, activation, one rounding (the conv output), the
-        //      residual added in fp32 and rounded again (nets/nn.py:49). The wave's 32 pixels x
-        //      32 couts go through its private LDS staging tile (lane (r32, h) writes its 16
-        //      couts, 4 lanes per pixel read 64 contiguous bytes back: every store instruction
-        //      writes 16 pixels x 64 B instead of 32 pixels x 2 x 16 B; conv_mx.hip co_stage)
-        if (kc == 0) {
-            int n, ty0, tx0;
-            tile_pos(it, n, ty0, tx0);
-            char* E = reinterpret_cast<char*>(sm4) + NS * SLOT + RED + (pg * NCG + cg) * 2048;
-            const int qr = lane & 3, pr0 = lane >> 2;
-#pragma unroll
-            for (int j = 0; j < MB; ++j) {
-#pragma unroll
-                for (int c = 0; c < 2; ++c) {
-                    unsigned w[4];
-#pragma unroll
-                    for (int e = 0; e < 8; e += 2) {
-                        float x0 = acc[j][8 * c + e] + bv[8 * c + e], x1 = acc[j][8 * c + e + 1] + bv[8 * c + e + 1];
-                        if (silu_act) {
-                            x0 = silu<T>(x0);
-                            x1 = silu<T>(x1);
-                        }
-                        w[e >> 1] = rw_pack2<T>(x0, x1);
-                    }
-                    const int q = 2 * h + c;
-                    *reinterpret_cast<uint4*>(E + (r32 * 4 + (q ^ ((r32 >> 1) & 3))) * 16) = make_uint4(w[0], w[1], w[2], w[3]);
-                }
-#pragma unroll
-                for (int k = 0; k < 2; ++k) {
-                    const int pp = k * 16 + pr0;
-                    const uint4 v = *reinterpret_cast<const uint4*>(E + (pp * 4 + (qr ^ ((pp >> 1) & 3))) * 16);
-                    unsigned w[4] = {v.x, v.y, v.z, v.w};
-                    const int px = (pg * MB + j) * 32 + pp;
-                    const int oy = ty0 + px / TW, ox = tx0 + px % TW;
-                    const bool ok = oy < p.Ho && ox < p.Wo;
-                    const long long m = ((long long)n * p.Ho + oy) * p.Wo + ox;
-                    if constexpr (RES) {
-                        const int f = (px >> RSH) & (RCH - 1);
-                        const char* rb = reinterpret_cast<const char*>(sm4) + (it % NS) * SLOT + NBI * NW * 1024 + px * RCH * 16;
-                        const uint4 r = *reinterpret_cast<const uint4*>(rb + ((cg * 4 + qr) ^ f) * 16);
-                        const unsigned rv[4] = {r.x, r.y, r.z, r.w};
-#pragma unroll
-                        for (int q = 0; q < 4; ++q)
-                            w[q] = rw_pack2<T>(rw_lo<T>(w[q]) + rw_lo<T>(rv[q]), rw_hi<T>(w[q]) + rw_hi<T>(rv[q]));
-                    }
-                    const unsigned oo = ok ? (unsigned)(m * p.ldo * 2) + (unsigned)(co0 + 8 * qr) * 2u : RW_OOB;
-                    const unsigned od = RW_DBG(8) ? RW_OOB : oo;
-                    __builtin_amdgcn_raw_buffer_store_b128(rw_u32x4{w[0], w[1], w[2], w[3]}, ro, od, 0, 0);
-                }
-            }
-        }
+        if (kc == 0) epilogue(it);
+
     }
     if (RW_TRACE && threadIdx.x == 0) {
         unsigned long long* tr = RW_TRACE + blockIdx.x * 4;
         tr[0] = t_entry; tr[1] = t_setup; tr[2] = t_first ? t_first : t_setup; tr[3] = __builtin_amdgcn_s_memrealtime();
+        if (RW_DBG(64)) tr[2] = t_setup + t_wait;   // "first" column = the summed loop-top waits
     }
 }
 
