@@ -98,13 +98,19 @@ def test_fused_stem_uint8_input(gpu, variant, dtype, batch, h, w):
     assert torch.equal(fused.forward(x8.to(dtype) / 255), yf)
 
 
-@pytest.mark.parametrize("dtype,batch,h,w,fits", [(torch.bfloat16, 2, 640, 640, True), (torch.float16, 3, 96, 160, True),
-                                                  (torch.bfloat16, 1, 1280, 1280, False)])
-def test_c3k_block_equals_per_layer_launches(gpu, dtype, batch, h, w, fits):
-    """c3k.hip: a CSPModule(128, 128) block (v11_n net.p5.1 / fpn.h6) in one launch per image
-    where the 20x20-stage image fits the LDS, the seven per-layer launches elsewhere (40x40 at
-    1280); YH_C3K=0 keeps the per-layer launches everywhere. Bit-identical either way."""
-    model = make_model("n")
+@pytest.mark.parametrize("variant,dtype,batch,h,w,nfused", [("n", torch.bfloat16, 2, 640, 640, 3),
+                                                           ("n", torch.float16, 3, 96, 160, 3),
+                                                           ("n", torch.bfloat16, 2, 608, 480, 3),
+                                                           ("n", torch.bfloat16, 1, 1280, 1280, 2),
+                                                           ("s", torch.float16, 2, 640, 640, 1),
+                                                           ("s", torch.bfloat16, 1, 1280, 1280, 0)])
+def test_c3k_block_equals_per_layer_launches(gpu, variant, dtype, batch, h, w, nfused):
+    """c3k.hip: a CSPModule(c, c) block with c = 64 or 128 in one launch wherever bands of at
+    least 4 rows (+ the 4-row halo) fit a workgroup's LDS: v11_n's 40x40 (c = 64) net.p4.1 and
+    20x20 (c = 128) net.p5.1 / fpn.h6 at 640, only the 40x40 c = 128 ones at 1280 (80x80 bands
+    are too wide); v11_s's 40x40 c = 128 net.p4.1 at 640 (its 20x20 blocks have c = 256), none
+    at 1280. YH_C3K=0 keeps the seven per-layer launches everywhere. Bit-identical either way."""
+    model = make_model(variant)
     x = synth.synth_scenes(batch, h, w, seed=37).to(gpu, dtype)
     fused = _engine(model, dtype, gpu, True)
     plain = _engine(model, dtype, gpu, True, YH_C3K="0")
@@ -113,9 +119,8 @@ def test_c3k_block_equals_per_layer_launches(gpu, dtype, batch, h, w, fits):
     kinds_f = [u["cls"] for u in fused.units(batch, h, w)]
     kinds_p = [u["cls"] for u in plain.units(batch, h, w)]
     assert "c3k" not in kinds_p
-    assert (kinds_f.count("c3k") == 2) == fits, kinds_f
-    if fits:   # seven launches -> one, twice
-        assert len(kinds_p) - len(kinds_f) == 12
+    assert kinds_f.count("c3k") == nfused, kinds_f
+    assert len(kinds_p) - len(kinds_f) == 6 * nfused   # seven launches -> one per fused block
     assert torch.isfinite(yf.float()).all()
     assert torch.equal(yf, yp), (yf.float() - yp.float()).abs().max().item()
 
@@ -172,8 +177,9 @@ def test_attention_lds_kernel_equals_per_wave_kernel(gpu, variant, dtype, batch,
 def test_c3k_row_bands_equal_per_layer_launches(gpu, bands):
     """c3k.hip row bands: each image's block is split over `bands` workgroups that recompute the
     4-row halo of the chain of four 3x3 convs; every split (1 = one workgroup per image, 20 =
-    one row each at 20x20, uneven splits, a last band with no rows) is bit-identical to the
-    seven per-layer launches. YH_C3K_BANDS is read at launch."""
+    one row each at 20x20, uneven splits, a last band with no rows; the 40x40 block takes at
+    least the 10 bands its regions need) is bit-identical to the seven per-layer launches.
+    YH_C3K_BANDS is read at launch."""
     model = make_model("n")
     x = synth.synth_scenes(2, 640, 640, seed=38).to(gpu, torch.bfloat16)
     plain = _engine(model, torch.bfloat16, gpu, True, YH_C3K="0")
@@ -189,5 +195,5 @@ def test_c3k_row_bands_equal_per_layer_launches(gpu, bands):
             del os.environ["YH_C3K_BANDS"]
         else:
             os.environ["YH_C3K_BANDS"] = old
-    assert [u["cls"] for u in fused.units(2, 640, 640)].count("c3k") == 2
+    assert [u["cls"] for u in fused.units(2, 640, 640)].count("c3k") == 3
     assert torch.equal(yf, yp), (yf.float() - yp.float()).abs().max().item()

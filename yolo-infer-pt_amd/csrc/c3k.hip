@@ -1,25 +1,26 @@
 // Fused C3k block (nets/nn.py:52-63, CSPModule(c, c) with two Residual(c/2, e=1.0)) for
-// the 16-bit handles, on maps small enough to keep a whole image's intermediates in LDS
-// (v11_n: net.p5.1.res_m.0 and fpn.h6.res_m.0 at 20x20, c = 128, h = c / 2 = 64).
+// the 16-bit handles, hidden width h = c / 2 = 32 or 64 (the HH template parameter), on maps
+// whose bands keep their intermediates in LDS (v11_n at 640 x 640: net.p4.1.res_m.0 at 40x40
+// with h = 32, net.p5.1.res_m.0 / fpn.h6.res_m.0 at 20x20 with h = 64).
 //
 // One workgroup (16 waves) per band of RB output rows of one image (the launcher cuts each
-// image into `bands` bands so that a batch fills the chip: one workgroup per image used 32 of
-// 256 CUs at batch 32). The chain of four 3x3 convs needs a 4-row halo: a workgroup keeps the
-// rows [r0 - 4, r1 + 4) of its band (clipped to the image) in LDS and each phase computes the
+// image into `bands` bands so that a batch fills the chip, and so that every band's region
+// fits). The chain of four 3x3 convs needs a 4-row halo: a workgroup keeps the rows
+// [r0 - 4, r1 + 4) of its band (clipped to the image) in LDS and each phase computes the
 // rows its successors read (B: halo 3, C: 2, D: 1, E and F: the band itself); pixels outside a
-// phase's rows are neither computed nor written. A 32-pixel tile per wave in every phase:
+// phase's rows are neither computed nor written. A 32-pixel tile per wave in every phase
+// (phase A also runs the region's bottom rows past the 16 waves' 512 pixels, conv1 only):
 //   A   C1 = conv1(x)            1x1 c -> h, + SiLU                   x from HBM -> LDS C1
 //   B   T  = r0.conv1(C1)        3x3 h -> h, + SiLU                   LDS -> LDS
 //   C   C1 = r0.conv2(T) + C1    3x3 h -> h, + SiLU, + residual       in place (nn.py:49)
 //   D   T  = r1.conv1(C1)
 //   E   C1 = r1.conv2(T) + C1
 //   F   y  = conv3([C1 | c2])    1x1 2h -> c, + SiLU             c2 = conv2(x), from phase A
-// Each 3x3 conv runs as two sub-phases, one per 32-cout tile; the tile's 36-step weight
-// image comes by LDS-DMA in two 18 KB halves that ping-pong between two buffers, the next
-// half in flight while the current one is multiplied (one copy per workgroup, read by every
-// wave, instead of one per wave). conv2
+// The 3x3 convs' weights (one 18-step image per 32-cout tile and pair of 16-channel blocks)
+// and then conv3's stream through a ring of 18 KB LDS buffers by LDS-DMA, several items
+// ahead of the one being multiplied (one copy per workgroup, read by every wave). conv2
 // never reaches LDS: its A rows are permuted (bits 2 and 3 swapped) so that a lane's
-// accumulator registers 8 jj .. 8 jj + 7 ARE conv3's B fragment of K block 4 + 2 t + jj.
+// accumulator registers 8 jj .. 8 jj + 7 ARE conv3's B fragment of K block h / 16 + 2 t + jj.
 //
 // Bit-identical to the per-layer conv_mx launches (conv_mx.h): every conv walks its K as
 // for 16-channel block: for tap: one v_mfma_f32_32x32x16 step, + bias, SiLU, one rounding
@@ -39,8 +40,7 @@ typedef __attribute__((ext_vector_type(2))) float ck_f32x2;
 
 constexpr int CK_NW = 16;                // waves per workgroup
 constexpr int CK_THREADS = 64 * CK_NW;
-constexpr int CK_H = 64;                 // hidden channels (h); c = 2h
-constexpr int CK_PX = 128;               // LDS bytes per pixel of C1 / T (64 channels)
+constexpr int CK_MINRB = 4;              // rows per band at least (the 4-row halo recomputation)
 
 template <typename T> struct KMfma;
 template <> struct KMfma<__bf16> {
@@ -79,15 +79,50 @@ __device__ __forceinline__ void ck_glds(const void* src, unsigned lds_addr) {
 }
 __device__ __forceinline__ void ck_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
-// swizzled 16-B chunk c of pixel p (C1 / T): 16 consecutive pixels hit 16 bank slots
-__device__ __forceinline__ int ck_off(int p, int c) { return p * CK_PX + ((c ^ ((p >> 1) & 7)) << 4); }
+// swizzled 16-B chunk c of pixel p (C1 / T, HH channels = HH / 8 chunks per pixel):
+// consecutive pixels spread over the bank slots
+template <int HH>
+__device__ __forceinline__ int ck_off(int p, int c) { return p * (2 * HH) + ((c ^ ((p >> 1) & (HH / 8 - 1))) << 4); }
 
 // 16 consecutive couts of one pixel (lane half h of a 32-cout tile, fragment rows as
 // c3k2.hip / conv_mx): bias, SiLU, one rounding -> 8 packed words
 template <typename T>
 __device__ __forceinline__ void ck_act(const f32x16& acc, const float* b, unsigned (&w)[8]) {
+    // 16 biases as four 16-B reads (b is 64-B aligned: 16 h floats past a 32-float boundary)
+    f32x4 bv[4];
 #pragma unroll
-    for (int e = 0; e < 16; e += 2) w[e >> 1] = ck_pack2<T>(silu<T>(acc[e] + b[e]), silu<T>(acc[e + 1] + b[e + 1]));
+    for (int i = 0; i < 4; ++i) bv[i] = reinterpret_cast<const f32x4*>(b)[i];
+#pragma unroll
+    for (int e = 0; e < 16; e += 2)
+        w[e >> 1] = ck_pack2<T>(silu<T>(acc[e] + bv[e >> 2][e & 3]), silu<T>(acc[e + 1] + bv[e >> 2][(e + 1) & 3]));
+}
+
+// 1x1 conv step chain of one 32-cout tile: NK K blocks, A fragments from LDS at w (read
+// CK_PF1 steps ahead of their MFMA, the order pinned through scheduling), B in registers
+#ifndef CK_PF1
+#define CK_PF1 4
+#endif
+template <typename T, int NK>
+__device__ __forceinline__ f32x16 ck_1x1(const char* w, int lane, const uint4 (&bv)[NK]) {
+    constexpr int PF = CK_PF1 < NK ? CK_PF1 : NK;
+    f32x16 acc;
+#pragma unroll
+    for (int e = 0; e < 16; ++e) acc[e] = 0.f;
+    uint4 fa[PF + 1];
+#pragma unroll
+    for (int st = 0; st < PF; ++st) fa[st] = *reinterpret_cast<const uint4*>(w + (st * 64 + lane) * 16);
+#pragma unroll
+    for (int st = 0; st < NK; ++st) {
+        if (st + PF < NK) fa[(st + PF) % (PF + 1)] = *reinterpret_cast<const uint4*>(w + ((st + PF) * 64 + lane) * 16);
+        acc = KMfma<T>::step(fa[st % (PF + 1)], bv[st], acc);
+    }
+    __builtin_amdgcn_sched_group_barrier(0x100, PF, 0);
+#pragma unroll
+    for (int st = 0; st < NK; ++st) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        if (st + PF < NK) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+    }
+    return acc;
 }
 
 }  // namespace
@@ -98,34 +133,86 @@ __host__ __device__ inline int ck_region_px(int H, int W, int bands) {
     return (rb + 8 < H ? rb + 8 : H) * W;
 }
 
-// parameter image (bytes): fragments [tile][step][64 lanes][16 B], then fp32 biases
+// parameter image (bytes) of a block with HH hidden channels (c = 2 HH): fragments
+// [tile][step][64 lanes][16 B], then fp32 biases
 struct CkLayout {
     int w1, w2, wr, w3, b1, b2, br, b3, total;
 };
+template <int HH>
 __host__ __device__ constexpr CkLayout ck_layout() {
+    constexpr int NT3 = HH / 32, NK1 = HH / 8, NK3 = 9 * (HH / 16), NTO = HH / 16;
     CkLayout L{};
-    L.w1 = 0;                              // conv1: 2 tiles x 8 K blocks
-    L.w2 = L.w1 + 2 * 8 * 1024;            // conv2: 2 x 8 (rows permuted for conv3's B fragments)
-    L.wr = L.w2 + 2 * 8 * 1024;            // 4 Residual convs: [conv][tile][36 steps]
-    L.w3 = L.wr + 4 * 2 * 36 * 1024;       // conv3: 4 tiles x 8 K blocks
-    L.b1 = L.w3 + 4 * 8 * 1024;
-    L.b2 = L.b1 + 64 * 4;
-    L.br = L.b2 + 64 * 4;                  // [conv][64]
-    L.b3 = L.br + 4 * 64 * 4;
-    L.total = L.b3 + 128 * 4;
+    L.w1 = 0;                                // conv1: NT3 tiles x NK1 K blocks (c -> h)
+    L.w2 = L.w1 + NT3 * NK1 * 1024;          // conv2: the same (rows permuted for conv3's B fragments)
+    L.wr = L.w2 + NT3 * NK1 * 1024;          // 4 Residual convs: [conv][tile][NK3 steps]
+    L.w3 = L.wr + 4 * NT3 * NK3 * 1024;      // conv3: NTO tiles x NK1 K blocks (2h -> c)
+    L.b1 = L.w3 + NTO * NK1 * 1024;
+    L.b2 = L.b1 + HH * 4;
+    L.br = L.b2 + HH * 4;                    // [conv][HH]
+    L.b3 = L.br + 4 * HH * 4;
+    L.total = L.b3 + 2 * HH * 4;
     return L;
 }
 
+// micro benchmark builds (tools/micro, -DYH_ABLATION): s_memrealtime stamps of wave 0 per
+// workgroup (0 entry, 1 prologue waited, 2 phase A done, 3 + i ring item i's barrier passed,
+// 3 + NITEMS exit); nothing in the shipped library
+constexpr int CK_NSTAMP = 24;
+#ifdef YH_ABLATION
+#define CK_STAMP(k)                                                                                       \
+    do {                                                                                                  \
+        if (A.trace && threadIdx.x == 0) A.trace[blockIdx.x * CK_NSTAMP + (k)] = __builtin_amdgcn_s_memrealtime(); \
+    } while (0)
+#else
+#define CK_STAMP(k) do { } while (0)
+#endif
+
 namespace {
 
-template <typename T>
+constexpr int CK_WBH = 18 * 1024;   // one weight buffer: 18 steps (two 16-channel blocks x 9 taps)
+constexpr int CK_IW = 9;            // waves that issue a ring item (2 x 1 KB each, uniform)
+constexpr int CK_MAXNB = 6;         // ring buffers at most
+#ifndef CK_PF
+#define CK_PF 3                     // 3x3 steps whose LDS reads are in flight ahead of the MFMA
+#endif
+
+// wait until at most k ring items (2 k LDS-DMA instructions) of this wave are in flight
+__device__ __forceinline__ void ck_wait_items(int k) {
+    switch (k) {
+        case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+        case 1: asm volatile("s_waitcnt vmcnt(2)" ::: "memory"); break;
+        case 2: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
+        case 3: asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); break;
+        case 4: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
+        default: asm volatile("s_waitcnt vmcnt(10)" ::: "memory"); break;
+    }
+}
+
+// LDS layout of a workgroup (bytes): C1 [rpx][hh], T [max(rpx hh, conv1 + conv2 weights)],
+// nb ring buffers of 18 KB, the zero block (128 B), the biases (32 hh B)
+__host__ __device__ inline int ck_tt_bytes(int hh, int rpx) {
+    const int w12 = 2 * (hh / 32) * (hh / 8) * 1024;
+    return rpx * 2 * hh > w12 ? rpx * 2 * hh : w12;
+}
+
+template <typename T, int HH>
 __global__ __launch_bounds__(CK_THREADS, 1) void c3k_fused(const C3kArgs A) {
-    constexpr CkLayout L = ck_layout();
-    constexpr int WBH = 18 * 1024;                   // one weight half (18 of a tile's 36 steps)
+    constexpr CkLayout L = ck_layout<HH>();
+    constexpr int PX = 2 * HH;                       // LDS bytes per pixel of C1 / T
+    constexpr int CPX = HH / 8;                      // 16-B chunks per pixel
+    constexpr int NT3 = HH / 32;                     // 32-cout tiles of conv1 / conv2 / the 3x3 convs
+    constexpr int NCB = HH / 16;                     // 16-channel blocks of h
+    constexpr int HALVES = NCB / 2;                  // ring items per 3x3 tile
+    constexpr int NK1 = HH / 8;                      // K blocks of conv1 / conv2 / conv3 (c = 2h inputs)
+    constexpr int NTO = HH / 16;                     // 32-cout tiles of conv3
+    constexpr int NHS = 4 * NT3 * HALVES;            // 3x3 sub-phases (one ring item each)
+    constexpr int W12 = NT3 * NK1 * 1024;            // conv1's (and conv2's) weight bytes
+    constexpr int W3 = NTO * NK1 * 1024;             // conv3's weight bytes
+    constexpr int TPG = 16 / NK1;                    // conv3 tiles per ring item (16 KB of it)
+    constexpr int NITEMS = NHS + (NTO + TPG - 1) / TPG;
     extern __shared__ __attribute__((aligned(1024))) char sm[];
     typedef __attribute__((address_space(3))) char* lds_c;
     const unsigned lds0 = (unsigned)(size_t)(lds_c)sm;
-    const int HW = A.H * A.W;
     // band rows [r0, r1) of image n; LDS region rows [ra0, ra1) (the band + its 4-row halo)
     const int n = blockIdx.x / A.bands, band = blockIdx.x - n * A.bands;
     const int RB = (A.H + A.bands - 1) / A.bands;
@@ -133,31 +220,49 @@ __global__ __launch_bounds__(CK_THREADS, 1) void c3k_fused(const C3kArgs A) {
     const int ra0 = max(0, r0 - 4), ra1 = min(A.H, r1 + 4);
     const int NRP = (ra1 - ra0) * A.W;               // region pixels
     const int RPX = ck_region_px(A.H, A.W, A.bands);   // LDS pixels per region image (the largest band's)
-    char* C1 = sm;                                   // [RPX][64] (swizzled chunks)
-    char* TT = sm + RPX * CK_PX;                     // [RPX][64]
-    const int wb_off = 2 * RPX * CK_PX;              // two weight halves
-    char* WB = sm + wb_off;
-    char* ZR = WB + 2 * WBH;                         // 128 zero bytes (out-of-image taps)
-    const float* BI = reinterpret_cast<const float*>(ZR + 128);   // every bias (2 KB)
+    const int NB = A.nbuf;                           // ring buffers (2 .. CK_MAXNB)
+    char* C1 = sm;                                   // [RPX][HH] (swizzled chunks)
+    char* TT = sm + RPX * PX;                        // [RPX][HH]; conv1 / conv2's weights before B
+    const int wb_off = RPX * PX + ck_tt_bytes(HH, RPX);
+    char* WB = sm + wb_off;                          // the ring
+    char* ZR = WB + NB * CK_WBH;                     // 128 zero bytes (out-of-image taps)
+    const float* BI = reinterpret_cast<const float*>(ZR + 128);   // every bias (32 HH bytes)
     const int lane = threadIdx.x & 63, l32 = lane & 31, h = lane >> 5;
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const char* prm = reinterpret_cast<const char*>(A.prm);
+    CK_STAMP(0);
     if (r0 >= A.H) return;   // workgroup-uniform (no band rows: nothing issued yet)
     // LDS-DMA of `kb` 1-KB pieces from the parameter image at `src` to LDS offset `dst`
     auto dma = [&](int src, int dst, int kb) {
         for (int i = wv; i < kb; i += CK_NW) ck_glds(prm + src + i * 1024 + lane * 16, lds0 + (unsigned)(dst + i * 1024));
     };
+    // ring item i -> buffer i % NB: the 3x3 sub-phases' 18-step weight images, then conv3's
+    // weights in 16 KB items; waves 0..8 issue two 1-KB pieces each (pieces past an item's
+    // end repeat its first piece into the buffer's unused tail), so every issuing wave has
+    // the same count in flight per item
+    auto issue = [&](int i) {
+        if (i >= NITEMS || wv >= CK_IW) return;   // wave-uniform
+        int src = L.wr + i * CK_WBH, np = 18;
+        if (i >= NHS) {
+            src = L.w3 + (i - NHS) * 16 * 1024;
+            np = min(16, (W3 - (i - NHS) * 16 * 1024) / 1024);
+        }
+        const unsigned dst = lds0 + (unsigned)(wb_off + (i % NB) * CK_WBH);
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+            const int pc = 2 * wv + k;
+            ck_glds(prm + src + (pc < np ? pc : 0) * 1024 + lane * 16, dst + (unsigned)(pc * 1024));
+        }
+    };
 
-    // prologue: conv1's weights into the second weight buffer, conv2's into T (free until the
-    // first Residual conv writes it) and the first 3x3 half into the first buffer; a region too
-    // small for conv2's 16 KB takes them in the first buffer, the 3x3 half then follows phase A
-    const bool w2_in_t = RPX * CK_PX >= 16 * 1024;   // uniform
-    dma(L.w1, wb_off + WBH, 16);
-    dma(L.w2, w2_in_t ? (int)(TT - sm) : wb_off, 16);
-    if (w2_in_t) dma(L.wr, wb_off, 18);
+    // prologue: conv1's and conv2's weights into T (free until the first Residual conv writes
+    // it), the biases; the x fragments of the wave's tile; the first NB - 1 ring items
+    dma(L.w1, (int)(TT - sm), 2 * W12 / 1024);       // w1, w2 are adjacent in the image
     dma(L.b1, (int)((const char*)BI - sm), (L.total - L.b1) / 1024);
     if (threadIdx.x < 8) *reinterpret_cast<uint4*>(ZR + threadIdx.x * 16) = make_uint4(0, 0, 0, 0);
-    // the wave's pixel tile: 32 consecutive region pixels (clamped; only p < NRP is written)
+    // the wave's pixel tile: 32 consecutive region pixels (clamped; only p < NRP is written).
+    // Phases B..F only reach the first 16 tiles (the launcher's bands guarantee it); region
+    // pixels past them (bottom halo rows of wide bands) get C1 from extra phase-A tiles.
     const int p = wv * 32 + l32;
     const bool own = wv * 32 < NRP;                  // wave-uniform: the wave has a tile
     const bool pv = p < NRP;
@@ -166,28 +271,46 @@ __global__ __launch_bounds__(CK_THREADS, 1) void c3k_fused(const C3kArgs A) {
     // rows of the wave's tile (wave-uniform): a phase runs the tile iff it meets the phase's rows
     const int ty0 = ra0 + (wv * 32) / A.W, ty1 = ra0 + (min(wv * 32 + 31, NRP - 1)) / A.W;
     auto live = [&](int lo, int hi) { return own && ty1 >= lo && ty0 < hi; };
-    const T* xp = reinterpret_cast<const T*>(A.x) + (((long long)n * A.H + py) * A.W + px) * A.ldx + 8 * h;
-    uint4 xb[8];
+    auto xrow = [&](int q) {
+        const int qy = ra0 + q / A.W, qx = q - (qy - ra0) * A.W;
+        return reinterpret_cast<const T*>(A.x) + (((long long)n * A.H + qy) * A.W + qx) * A.ldx + 8 * h;
+    };
+    uint4 xb[NK1];
+    {
+        const T* xp = xrow(pc);
 #pragma unroll
-    for (int kb = 0; kb < 8; ++kb) xb[kb] = *reinterpret_cast<const uint4*>(xp + 16 * kb);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        for (int kb = 0; kb < NK1; ++kb) xb[kb] = *reinterpret_cast<const uint4*>(xp + 16 * kb);
+    }
+    for (int i = 0; i < NB - 1; ++i) issue(i);
+    if (wv < CK_IW) ck_wait_items(min(NB - 1, NITEMS));   // all but the ring items
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     ck_barrier();
+    CK_STAMP(1);
 
     // ---- A: C1 = SiLU(conv1(x)) -> LDS; conv2(x) -> registers (its rows permuted: registers
     //      8 jj .. + 7 of tile t are channels 32 t + 16 jj + 8 h .. + 7 = conv3's B fragment of
-    //      K block 4 + 2 t + jj), held until phase F. B fragments from HBM, A from LDS.
-    uint4 bf[8];
+    //      K block NCB + 2 t + jj), held until phase F. B fragments from HBM, A from LDS.
+    uint4 bf[NK1];
     f32x16 acc;
+    auto conv1_tile = [&](int q, bool qv) {
+        const char* w1 = TT;
+#pragma unroll
+        for (int t = 0; t < NT3; ++t) {
+            const f32x16 a1 = ck_1x1<T, NK1>(w1 + t * NK1 * 1024, lane, xb);
+            unsigned w[8];
+            ck_act<T>(a1, BI + 32 * t + 16 * h, w);
+            if (qv) {
+                *reinterpret_cast<uint4*>(C1 + ck_off<HH>(q, 4 * t + 2 * h)) = make_uint4(w[0], w[1], w[2], w[3]);
+                *reinterpret_cast<uint4*>(C1 + ck_off<HH>(q, 4 * t + 2 * h + 1)) = make_uint4(w[4], w[5], w[6], w[7]);
+            }
+        }
+    };
     if (own) {
-        const char* w2 = w2_in_t ? TT : WB;
+        const char* w2 = TT + W12;
         const float* b2 = BI + (L.b2 - L.b1) / 4;
 #pragma unroll
-        for (int t = 0; t < 2; ++t) {
-#pragma unroll
-            for (int e = 0; e < 16; ++e) acc[e] = 0.f;
-#pragma unroll
-            for (int kb = 0; kb < 8; ++kb)
-                acc = KMfma<T>::step(*reinterpret_cast<const uint4*>(w2 + ((t * 8 + kb) * 64 + lane) * 16), xb[kb], acc);
+        for (int t = 0; t < NT3; ++t) {
+            acc = ck_1x1<T, NK1>(w2 + t * NK1 * 1024, lane, xb);
 #pragma unroll
             for (int jj = 0; jj < 2; ++jj) {
                 const float* bj = b2 + 32 * t + 16 * jj + 8 * h;
@@ -195,33 +318,23 @@ __global__ __launch_bounds__(CK_THREADS, 1) void c3k_fused(const C3kArgs A) {
 #pragma unroll
                 for (int e = 0; e < 8; e += 2)
                     w[e >> 1] = ck_pack2<T>(silu<T>(acc[8 * jj + e] + bj[e]), silu<T>(acc[8 * jj + e + 1] + bj[e + 1]));
-                bf[4 + 2 * t + jj] = make_uint4(w[0], w[1], w[2], w[3]);
+                bf[NCB + 2 * t + jj] = make_uint4(w[0], w[1], w[2], w[3]);
             }
         }
-        const char* w1 = WB + WBH;
-#pragma unroll
-        for (int t = 0; t < 2; ++t) {
-            f32x16 acc;
-#pragma unroll
-            for (int e = 0; e < 16; ++e) acc[e] = 0.f;
-#pragma unroll
-            for (int kb = 0; kb < 8; ++kb)
-                acc = KMfma<T>::step(*reinterpret_cast<const uint4*>(w1 + ((t * 8 + kb) * 64 + lane) * 16), xb[kb], acc);
-            unsigned w[8];
-            ck_act<T>(acc, BI + 32 * t + 16 * h, w);
-            if (pv) {
-                *reinterpret_cast<uint4*>(C1 + ck_off(p, 4 * t + 2 * h)) = make_uint4(w[0], w[1], w[2], w[3]);
-                *reinterpret_cast<uint4*>(C1 + ck_off(p, 4 * t + 2 * h + 1)) = make_uint4(w[4], w[5], w[6], w[7]);
-            }
-        }
+        conv1_tile(p, pv);
     }
-    if (!w2_in_t) {
-        ck_barrier();   // conv2's weights read: the first 3x3 half may land in the first buffer
-        dma(L.wr, wb_off, 18);
+    for (int q0 = wv * 32 + 32 * CK_NW; q0 < NRP; q0 += 32 * CK_NW) {   // wave-uniform
+        const int q = q0 + l32;
+        const bool qv = q < NRP;
+        const T* xq = xrow(qv ? q : NRP - 1);
+#pragma unroll
+        for (int kb = 0; kb < NK1; ++kb) xb[kb] = *reinterpret_cast<const uint4*>(xq + 16 * kb);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // (ring items too: rare, harmless)
+        conv1_tile(q, qv);
     }
 
     // 3x3 taps of the wave's pixel: pixel byte offset within C1 / T with the chunk swizzle in
-    // its low bits (-128: outside the image, read from the zero block)
+    // its low bits (-PX: outside the image, read from the zero block)
     int tq[9];
 #pragma unroll
     for (int t = 0; t < 9; ++t) {
@@ -230,53 +343,94 @@ __global__ __launch_bounds__(CK_THREADS, 1) void c3k_fused(const C3kArgs A) {
         // outputs no later phase reads): the zero block too
         const bool in = yy >= ra0 && yy < ra1 && (unsigned)xx < (unsigned)A.W;
         const int q = (yy - ra0) * A.W + xx;
-        tq[t] = in ? (q * CK_PX) | ((q >> 1) & 7) : -CK_PX;
+        tq[t] = in ? (q * PX) | ((q >> 1) & (CPX - 1)) : -PX;
     }
     const int zr_off = (int)(ZR - sm);
+    CK_STAMP(2);
+    const float* b3 = BI + (L.b3 - L.b1) / 4;
+    T* y = reinterpret_cast<T*>(A.y) + (((long long)n * A.H + py) * A.W + px) * A.ldy;
+    const bool fl = live(r0, r1);
 
-    // ---- B..E: the Residual convs, one 32-cout tile per sub-phase. A tile's 36 weight steps
-    //      arrive as two 18 KB halves that ping-pong between two LDS buffers: the next half
-    //      (of this tile or the next one; after the last one, conv3's first two tiles) is
-    //      DMA'd while the current half is multiplied.
+    // ---- B..E: the Residual convs, one 32-cout tile per NCB / 2 ring items (18 weight steps
+    //      each); F: conv3 over [C1 | conv2] -> y, TPG tiles per ring item. Item i is in
+    //      buffer i % NB; items i + 1 .. i + NB - 2 are in flight while it is multiplied, and
+    //      item i + NB - 1 is issued into the buffer item i - 1 used.
 #pragma unroll 1
-    for (int hs = 0; hs < 16; ++hs) {
-        const int cv = hs >> 2, t = (hs >> 1) & 1, half = hs & 1;
+    for (int i = 0; i < NITEMS; ++i) {
+        if (wv < CK_IW) ck_wait_items(min(NB - 2, NITEMS - 1 - i));   // this wave's pieces of item i
+        ck_barrier();   // ... and everyone's; item i - 1's buffer and the previous phase are done
+        CK_STAMP(3 + i);
+        issue(i + NB - 1);
+        const char* wb = WB + (i % NB) * CK_WBH;
+        if (i >= NHS) {
+            // ---- F
+            if (!fl) continue;
+            if (i == NHS) {
+#pragma unroll
+                for (int kb = 0; kb < NCB; ++kb) bf[kb] = *reinterpret_cast<const uint4*>(C1 + ck_off<HH>(pc, 2 * kb + h));
+            }
+            const int g = i - NHS;
+#pragma unroll
+            for (int tt = 0; tt < TPG; ++tt) {
+                const int t = g * TPG + tt;
+                if (t >= NTO) break;
+                const char* w3 = wb + tt * NK1 * 1024;
+                acc = ck_1x1<T, NK1>(w3, lane, bf);
+                unsigned w[8];
+                ck_act<T>(acc, b3 + 32 * t + 16 * h, w);
+                if (pv && py >= r0 && py < r1) {
+                    uint4* d = reinterpret_cast<uint4*>(y + 32 * t + 16 * h);
+                    d[0] = make_uint4(w[0], w[1], w[2], w[3]);
+                    d[1] = make_uint4(w[4], w[5], w[6], w[7]);
+                }
+            }
+            continue;
+        }
+        const int cv = i / (NT3 * HALVES), t = (i / HALVES) % NT3, half = i % HALVES;
         char* src = (cv & 1) ? TT : C1;
         char* dst = (cv & 1) ? C1 : TT;
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's DMAs of half-step hs
-        ck_barrier();   // ... and everyone's; the other buffer and the previous phase are done
-        if (hs + 1 < 16) dma(L.wr + (hs + 1) * WBH, wb_off + ((hs + 1) & 1) * WBH, 18);
-        else dma(L.w3, wb_off, 16);
         // rows this conv must produce: the band + (3 - cv) halo rows (what conv cv + 1 reads)
         const int lo = max(0, r0 - (3 - cv)), hi = min(A.H, r1 + (3 - cv));
         if (!live(lo, hi)) continue;
         const int src_off = (int)(src - sm);
         int tb[9];
 #pragma unroll
-        for (int k = 0; k < 9; ++k) tb[k] = tq[k] >= 0 ? src_off + (tq[k] & ~(CK_PX - 1)) : zr_off;
+        for (int k = 0; k < 9; ++k) tb[k] = tq[k] >= 0 ? src_off + (tq[k] & ~(PX - 1)) : zr_off;
         if (half == 0) {
 #pragma unroll
             for (int e = 0; e < 16; ++e) acc[e] = 0.f;
         }
-        const char* wb = WB + half * WBH;
-#pragma unroll 1
-        for (int cb = 2 * half; cb < 2 * half + 2; ++cb)
+        // the item's 18 steps (16-channel blocks 2 half, 2 half + 1; 9 taps each), software
+        // pipelined: step s + CK_PF's A / B fragments are read while step s multiplies
+        uint4 fa[CK_PF + 1], fb[CK_PF + 1];
+        auto ld = [&](int st) {
+            const int j = st / 9, k = st - 9 * j, cb = 2 * half + j;
+            fa[st % (CK_PF + 1)] = *reinterpret_cast<const uint4*>(wb + ((j * 9 + k) * 64 + lane) * 16);
+            fb[st % (CK_PF + 1)] = *reinterpret_cast<const uint4*>(sm + tb[k] + (((2 * cb + h) ^ (tq[k] & (CPX - 1))) << 4));
+        };
 #pragma unroll
-            for (int k = 0; k < 9; ++k) {
-                const uint4 a = *reinterpret_cast<const uint4*>(wb + (((cb & 1) * 9 + k) * 64 + lane) * 16);
-                const uint4 b = *reinterpret_cast<const uint4*>(sm + tb[k] + (((2 * cb + h) ^ (tq[k] & 7)) << 4));
-                acc = KMfma<T>::step(a, b, acc);
-                if (k % 3 == 2) asm volatile("" ::: "memory");   // 3 taps' reads in flight (VGPR budget)
-            }
-        if (half == 0) continue;
+        for (int st = 0; st < CK_PF; ++st) ld(st);
+#pragma unroll
+        for (int st = 0; st < 18; ++st) {
+            if (st + CK_PF < 18) ld(st + CK_PF);
+            acc = KMfma<T>::step(fa[st % (CK_PF + 1)], fb[st % (CK_PF + 1)], acc);
+        }
+        // keep that order through scheduling (it would otherwise sink the reads to one step ahead)
+        __builtin_amdgcn_sched_group_barrier(0x100, 2 * CK_PF, 0);
+#pragma unroll
+        for (int st = 0; st < 18; ++st) {
+            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+            if (st + CK_PF < 18) __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+        }
+        if (half != HALVES - 1) continue;
         unsigned w[8];
-        ck_act<T>(acc, BI + (L.br - L.b1) / 4 + 64 * cv + 32 * t + 16 * h, w);
+        ck_act<T>(acc, BI + (L.br - L.b1) / 4 + HH * cv + 32 * t + 16 * h, w);
         if (pv && py >= lo && py < hi) {
-            const int o0 = ck_off(p, 4 * t + 2 * h), o1 = ck_off(p, 4 * t + 2 * h + 1);
+            const int o0 = ck_off<HH>(p, 4 * t + 2 * h), o1 = ck_off<HH>(p, 4 * t + 2 * h + 1);
             if (cv & 1) {   // conv2 of a Residual: + its input (C1), rounded again (nn.py:49)
-                const uint4 r0 = *reinterpret_cast<const uint4*>(C1 + o0);
-                const uint4 r1 = *reinterpret_cast<const uint4*>(C1 + o1);
-                const unsigned rv[8] = {r0.x, r0.y, r0.z, r0.w, r1.x, r1.y, r1.z, r1.w};
+                const uint4 q0 = *reinterpret_cast<const uint4*>(C1 + o0);
+                const uint4 q1 = *reinterpret_cast<const uint4*>(C1 + o1);
+                const unsigned rv[8] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w};
 #pragma unroll
                 for (int q = 0; q < 8; ++q) w[q] = ck_pack2<T>(ck_lo<T>(w[q]) + ck_lo<T>(rv[q]), ck_hi<T>(w[q]) + ck_hi<T>(rv[q]));
             }
@@ -284,96 +438,99 @@ __global__ __launch_bounds__(CK_THREADS, 1) void c3k_fused(const C3kArgs A) {
             *reinterpret_cast<uint4*>(dst + o1) = make_uint4(w[4], w[5], w[6], w[7]);
         }
     }
-    // ---- F: conv3 over [C1 | conv2] -> y; its tiles 0-1 from the first buffer (landed during
-    //      the last half-step), tiles 2-3 from the second (DMA'd now, while 0-1 multiply)
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    ck_barrier();
-    dma(L.w3 + 16 * 1024, wb_off + WBH, 16);
-    const float* b3 = BI + (L.b3 - L.b1) / 4;
-    T* y = reinterpret_cast<T*>(A.y) + (((long long)n * A.H + py) * A.W + px) * A.ldy;
-    const bool fl = live(r0, r1);
-    if (fl) {
-#pragma unroll
-        for (int kb = 0; kb < 4; ++kb) bf[kb] = *reinterpret_cast<const uint4*>(C1 + ck_off(pc, 2 * kb + h));
-    }
-#pragma unroll
-    for (int t = 0; t < 4; ++t) {
-        if (t == 2) {
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            ck_barrier();
-        }
-        if (!fl) continue;
-        const char* w3 = WB + (t >> 1) * WBH + (t & 1) * 8 * 1024;
-#pragma unroll
-        for (int e = 0; e < 16; ++e) acc[e] = 0.f;
-#pragma unroll
-        for (int kb = 0; kb < 8; ++kb)
-            acc = KMfma<T>::step(*reinterpret_cast<const uint4*>(w3 + (kb * 64 + lane) * 16), bf[kb], acc);
-        unsigned w[8];
-        ck_act<T>(acc, b3 + 32 * t + 16 * h, w);
-        if (pv && py >= r0 && py < r1) {
-            uint4* d = reinterpret_cast<uint4*>(y + 32 * t + 16 * h);
-            d[0] = make_uint4(w[0], w[1], w[2], w[3]);
-            d[1] = make_uint4(w[4], w[5], w[6], w[7]);
-        }
-    }
+    CK_STAMP(3 + NITEMS);
 }
 
-// LDS bytes for region images of rpx pixels: C1 + T, two 18 KB weight halves (also conv1 /
-// conv2 / conv3's 32 KB), the zero block, the biases
-static long long ck_lds_px(long long rpx) {
-    return 2 * rpx * CK_PX + 36 * 1024 + 128 + (ck_layout().total - ck_layout().b1);
+// LDS bytes of a workgroup with region images of rpx pixels and nb ring buffers
+static long long ck_lds_px(int hh, long long rpx, int nb) {
+    return rpx * 2 * hh + ck_tt_bytes(hh, (int)rpx) + (long long)nb * CK_WBH + 128 + 32 * hh;
 }
 
-template <typename T>
+// pixels from a band region's first row to the last row phases B..F use (the band + 3 halo
+// rows below, 4 above): they must lie in the 16 waves' tiles
+static int ck_live_px(int H, int W, int bands) {
+    const int rb = (H + bands - 1) / bands;
+    return std::min(rb + 7, H) * W;
+}
+
+// bands per image: start from `r` and add bands until the phases' pixels fit 16 waves'
+// tiles, the region two passes of them, and the LDS two ring buffers (at most one row per band)
+static int ck_fit_bands(int hh, int H, int W, int r) {
+    auto fits = [&](int b) {
+        const int rpx = ck_region_px(H, W, b);
+        return ck_live_px(H, W, b) <= 32 * CK_NW && rpx <= 2 * 32 * CK_NW && ck_lds_px(hh, rpx, 2) <= 160 * 1024;
+    };
+    r = std::max(1, std::min(r, H));
+    while (r < H && !fits(r)) ++r;
+    return r;
+}
+
+template <typename T, int HH>
 int launch_c3k_t(const C3kArgs& a0, hipStream_t s) {
     C3kArgs a = a0;
-    a.bands = c3k_bands(a.B, a.H, a.W);
-    const long long lds = ck_lds_px(ck_region_px(a.H, a.W, a.bands));
-    if (c3k_lds(a.H, a.W) == 0 || lds > 160 * 1024 || a.B < 1 || a.ldx % 8 || a.ldy % 8)
+    a.bands = c3k_bands(a.B, a.H, a.W, HH);
+    const int rpx = ck_region_px(a.H, a.W, a.bands);
+    // as many ring buffers as the LDS holds (YH_C3K_NB: fewer)
+    a.nbuf = 2;
+    while (a.nbuf < CK_MAXNB && ck_lds_px(HH, rpx, a.nbuf + 1) <= 160 * 1024) ++a.nbuf;
+    if (const char* e = getenv("YH_C3K_NB")) a.nbuf = std::max(2, std::min(a.nbuf, atoi(e)));
+    const long long lds = ck_lds_px(HH, rpx, a.nbuf);
+    if (c3k_lds(a.H, a.W, HH) == 0 || ck_live_px(a.H, a.W, a.bands) > 32 * CK_NW || rpx > 2 * 32 * CK_NW ||
+        lds > 160 * 1024 || a.B < 1 || a.ldx % 8 || a.ldy % 8)
         return (int)hipErrorInvalidValue;
     static bool attr = false;
     if (!attr) {
-        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&c3k_fused<T>), hipFuncAttributeMaxDynamicSharedMemorySize,
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&c3k_fused<T, HH>), hipFuncAttributeMaxDynamicSharedMemorySize,
                                   160 * 1024);
         attr = true;
     }
-    hipLaunchKernelGGL((c3k_fused<T>), dim3((unsigned)(a.B * a.bands)), dim3(CK_THREADS), (int)lds, s, a);
+    hipLaunchKernelGGL((c3k_fused<T, HH>), dim3((unsigned)(a.B * a.bands)), dim3(CK_THREADS), (int)lds, s, a);
     return (int)hipGetLastError();
 }
 
 }  // namespace
 
-int c3k_prm_bytes() { return ck_layout().total; }
+int c3k_prm_bytes(int hh) {
+    return hh == 32 ? ck_layout<32>().total : hh == 64 ? ck_layout<64>().total : 0;
+}
 
-void c3k_offsets(int (&off)[9]) {
-    const CkLayout L = ck_layout();
+void c3k_offsets(int hh, int (&off)[9]) {
+    const CkLayout L = hh == 32 ? ck_layout<32>() : ck_layout<64>();
     const int v[9] = {L.w1, L.w2, L.wr, L.w3, L.b1, L.b2, L.br, L.b3, L.total};
     for (int i = 0; i < 9; ++i) off[i] = v[i];
 }
 
-int c3k_lds(int H, int W) {
-    const long long hw = (long long)H * W;
-    if (H < 1 || W < 1 || hw > 32 * CK_NW) return 0;
-    const long long b = ck_lds_px(hw);
+int c3k_lds(int H, int W, int hh) {
+    if (H < 1 || W < 1 || (hh != 32 && hh != 64)) return 0;
+    // the fewest bands that fit; bands of fewer than CK_MINRB rows recompute too much halo
+    const int r = ck_fit_bands(hh, H, W, 1);
+    const int rpx = ck_region_px(H, W, r);
+    if (ck_live_px(H, W, r) > 32 * CK_NW || rpx > 2 * 32 * CK_NW || (r > 1 && (H + r - 1) / r < CK_MINRB)) return 0;
+    const long long b = ck_lds_px(hh, rpx, 2);
     return b <= 160 * 1024 ? (int)b : 0;
 }
 
 int c3k_region_px(int H, int W, int bands) { return ck_region_px(H, W, bands); }
 
-int c3k_bands(int B, int H, int W) {
-    // enough workgroups for the chip (>= 128) with bands of >= 4 rows; YH_C3K_BANDS overrides
-    int r = std::max(1, std::min((128 + B - 1) / B, H / 4));
+int c3k_bands(int B, int H, int W, int hh) {
+    // enough workgroups for the chip (>= 128) with bands of >= CK_MINRB rows, then as many
+    // more as the regions need to fit; YH_C3K_BANDS overrides the first choice
+    int r = std::max(1, std::min((128 + B - 1) / B, H / CK_MINRB));
     if (const char* e = getenv("YH_C3K_BANDS")) r = std::max(1, std::min(atoi(e), H));
-    while (r > 1 && ck_region_px(H, W, r) > 32 * CK_NW) --r;   // never: a band region <= the image
-    (void)W;
-    return r;
+    return ck_fit_bands(hh, H, W, r);
 }
 
 int launch_c3k(int dtype, const C3kArgs& a, hipStream_t s) {
-    switch (dtype) {
-        case F16: return launch_c3k_t<_Float16>(a, s);
-        case BF16: return launch_c3k_t<__bf16>(a, s);
+    if (a.hh == 32) {
+        switch (dtype) {
+            case F16: return launch_c3k_t<_Float16, 32>(a, s);
+            case BF16: return launch_c3k_t<__bf16, 32>(a, s);
+        }
+    } else if (a.hh == 64) {
+        switch (dtype) {
+            case F16: return launch_c3k_t<_Float16, 64>(a, s);
+            case BF16: return launch_c3k_t<__bf16, 64>(a, s);
+        }
     }
     return (int)hipErrorInvalidValue;
 }

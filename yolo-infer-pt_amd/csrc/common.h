@@ -168,20 +168,25 @@ constexpr int HEAD_CLS_LDS = YH_HEAD_CLS_LDS_KB * 1024;   // 80: two workgroups 
 int head_cls_lds(int TH, int TW, int C0, int c3, int nc);
 int launch_head_cls(int dtype, const HeadClsArgs& a, hipStream_t s);
 
-// Fused C3k block (c3k.hip; nets/nn.py:52-63 CSPModule(c, c), c = 128, two Residual(64,
-// e=1.0)): one workgroup per image, every intermediate in LDS. Images of at most 512
-// pixels (v11_n's 20x20 stage at 640 x 640); bit-identical to the seven per-layer launches.
+// Fused C3k block (c3k.hip; nets/nn.py:52-63 CSPModule(c, c), c = 2 hh, two Residual(hh,
+// e=1.0), hh = 32 or 64): every intermediate of a band of rows (+ the 4-row halo of the four
+// 3x3 convs) in one workgroup's LDS. Maps whose bands of >= 4 rows keep <= 512 pixels (v11_n's
+// 40x40 hh = 32 and 20x20 hh = 64 blocks at 640 x 640); bit-identical to the seven
+// per-layer launches.
 struct C3kArgs {
     const void* x; int ldx;          // block input (NHWC view, c channels)
     void* y; int ldy;                // block output view (c channels)
     int B, H, W;
     const void* prm;                 // packed parameters (c3k_offsets)
+    int hh;                          // hidden channels (32 or 64)
     int bands;                       // row bands per image (set by launch_c3k: c3k_bands)
+    int nbuf;                        // weight ring buffers (set by launch_c3k)
+    unsigned long long* trace;       // micro benchmark builds (YH_ABLATION): per-workgroup stamps
 };
-int c3k_prm_bytes();
-void c3k_offsets(int (&off)[9]);     // w1, w2, residual convs, w3, b1, b2, residual biases, b3, total
-int c3k_lds(int H, int W);           // 0: the image does not fit
-int c3k_bands(int B, int H, int W);  // row bands per image (one workgroup each)
+int c3k_prm_bytes(int hh);
+void c3k_offsets(int hh, int (&off)[9]);   // w1, w2, residual convs, w3, b1, b2, residual biases, b3, total
+int c3k_lds(int H, int W, int hh);   // 0: no band split fits
+int c3k_bands(int B, int H, int W, int hh);   // row bands per image (one workgroup each)
 int c3k_region_px(int H, int W, int bands);   // LDS pixels of a band's region (band + 4-row halo)
 int launch_c3k(int dtype, const C3kArgs& a, hipStream_t s);
 

@@ -306,7 +306,7 @@ struct Net {
         // c3k.hip moves 8 channels per 16-byte access at ptr(view) + 8 h: both views must start
         // on an 8-channel boundary (slice() enforces it today; checked here so the op never
         // depends on that)
-        if (dtype != F32 && opt.fuse && opt.c3k && in_ch == 128 && out_ch == 128 && x.C == 128 &&
+        if (dtype != F32 && opt.fuse && opt.c3k && (in_ch == 64 || in_ch == 128) && out_ch == in_ch && x.C == in_ch &&
             x.coff % 8 == 0 && out.coff % 8 == 0) {
             Op op;
             op.kind = OP_C3K;
@@ -687,8 +687,11 @@ struct Net {
             d0.mx_w.erase(it);
         }
         for (int k = 0; k < 7; ++k) require(convs[op.ck[k]].loaded, "weights of " + convs[op.ck[k]].name + " not loaded", YH_ESTATE);
+        // hidden channels hh = conv1's couts (32 or 64): NT3 = hh / 32 tiles of conv1 / conv2 /
+        // the 3x3 convs over hh / 8 (1x1) or 9 hh / 16 (3x3) K steps, conv3: hh / 16 tiles
+        const int hh = convs[op.ck[0]].cout, nt3 = hh / 32, nk1 = hh / 8, nk3 = 9 * hh / 16;
         int off[9];
-        c3k_offsets(off);
+        c3k_offsets(hh, off);
         std::vector<uint8_t> img((size_t)off[8], 0);
         // fragment (tile a, step k, lane, j); rows: lane half hh of tile a holds couts
         // 32a + 16hh .. +15 (c3k2.hip's order), or with bits 2 and 3 of the row swapped (rho:
@@ -709,17 +712,17 @@ struct Net {
                             dst[((size_t)(a * nk + k) * 64 + lane) * 8 + j] = dtype == BF16 ? f2bf(v) : f2h(v);
                         }
         };
-        frags(off[0], convs[op.ck[0]], 2, 8, false);
-        frags(off[1], convs[op.ck[1]], 2, 8, true);
-        for (int r = 0; r < 4; ++r) frags(off[2] + r * 2 * 36 * 1024, convs[op.ck[2 + r]], 2, 36, false);
-        frags(off[3], convs[op.ck[6]], 4, 8, false);
+        frags(off[0], convs[op.ck[0]], nt3, nk1, false);
+        frags(off[1], convs[op.ck[1]], nt3, nk1, true);
+        for (int r = 0; r < 4; ++r) frags(off[2] + r * nt3 * nk3 * 1024, convs[op.ck[2 + r]], nt3, nk3, false);
+        frags(off[3], convs[op.ck[6]], hh / 16, nk1, false);
         auto biases = [&](int o, const ConvDesc& d) {
             float* dst = reinterpret_cast<float*>(img.data() + o);
             for (int i = 0; i < d.cout; ++i) dst[i] = d.bf[i];
         };
         biases(off[4], convs[op.ck[0]]);
         biases(off[5], convs[op.ck[1]]);
-        for (int r = 0; r < 4; ++r) biases(off[6] + r * 64 * 4, convs[op.ck[2 + r]]);
+        for (int r = 0; r < 4; ++r) biases(off[6] + r * hh * 4, convs[op.ck[2 + r]]);
         biases(off[7], convs[op.ck[6]]);
         void* dev = nullptr;
         HIPCHECK(hipMalloc(&dev, img.size()));
@@ -1371,6 +1374,7 @@ struct Net {
                 a.W = W >> lv;
                 a.B = B;
                 a.prm = c3k_params(op);
+                a.hh = convs[op.ck[0]].cout;
                 rc = launch_c3k(dtype, a, s);
                 break;
             }
@@ -1389,13 +1393,13 @@ struct Net {
         auto it = plans.find(key);
         if (it != plans.end()) { cur_plan = &it->second; return; }
         Plan pl;
-        // a fused C3k block runs where one image fits a workgroup's LDS (c3k_lds), its seven
-        // per-layer launches everywhere else
+        // a fused C3k block runs where bands of its map fit a workgroup's LDS (c3k_lds), its
+        // seven per-layer launches everywhere else
         pl.active.assign(ops.size(), 1);
         for (size_t i = 0; i < ops.size(); ++i) {
             if (ops[i].kind != OP_C3K) continue;
             const int lv = tensors[ops[i].out.t].level;
-            if (c3k_lds(H >> lv, W >> lv) > 0)
+            if (c3k_lds(H >> lv, W >> lv, convs[ops[i].ck[0]].cout) > 0)
                 for (int k = ops[i].alt0; k < ops[i].alt1; ++k) pl.active[k] = 0;
             else
                 pl.active[i] = 0;
