@@ -92,10 +92,21 @@ __host__ __device__ inline HcLayout hc_layout(int TH, int TW, int C0, int c3) {
 // pixels, stride ss, channel offset 0 = c_lo) into `dst` (DH x DW pixels, stride ds, channel
 // offset c_lo). An item is (4-channel group, column, block of HC_RB rows): its (HC_RB + 2) x 3
 // input pixels are read once and every output row has its own FMA chain (taps row-major).
+// floor(n / d) as (n * m) >> s with m = floor(2^s / d) + 1: exact for 0 <= n < 2^s / d (and
+// n * m < 2^32), which the tile index ranges here satisfy (tiles of at most 24 x 36 pixels)
+struct HcDiv {
+    unsigned m;
+    int s;
+};
+__device__ __forceinline__ HcDiv hc_div(int d, int s) { return HcDiv{(1u << s) / (unsigned)d + 1u, s}; }
+__device__ __forceinline__ int hc_q(int n, HcDiv f) { return (int)(((unsigned)n * f.m) >> f.s); }
+
 template <typename T>
 __device__ __forceinline__ void hc_dw(const T* src, int SW, int ss, T* dst, int DH, int DW, int ds, int c_lo, int C,
                                       const float* w, int wld, const float* b) {
     const int nrb = (DH + HC_RB - 1) / HC_RB, per_g = DW * nrb, ng = C >> 2;
+    const HcDiv dg = hc_div(per_g, 24), dw = hc_div(DW, 16);   // q < 2^24 / per_g: ng <= 64 groups
+    const int rs = SW * ss;                                      // one source row (elements)
     // the first item's weights are loaded before the barrier that opens the phase
     float4 wt[9], bb;
     int wg = -1;
@@ -109,18 +120,20 @@ __device__ __forceinline__ void hc_dw(const T* src, int SW, int ss, T* dst, int 
     hc_barrier();   // src (and the parameters in LDS) complete
     if ((int)threadIdx.x < ng * per_g) load_w(threadIdx.x / per_g);
     for (int q = threadIdx.x; q < ng * per_g; q += HEAD_CLS_THREADS) {
-        const int g = q / per_g, rem = q - g * per_g;
-        const int rb = rem / DW, c = rem - rb * DW;
+        const int g = hc_q(q, dg), rem = q - g * per_g;
+        const int rb = hc_q(rem, dw), c = rem - rb * DW;
         const int r0 = rb * HC_RB, c0 = c_lo + g * 4;
         if (g != wg) load_w(g);
+        // rows past the source's last (DH + 1) read that row (outputs discarded below)
+        const T* sp = src + (r0 * SW + c) * ss + g * 4;
+        const int lim = DH + 1 - r0, lim_off = lim * rs;
         uint2 xv[HC_RB + 2][3];
 #pragma unroll
-        for (int r = 0; r < HC_RB + 2; ++r)
+        for (int r = 0; r < HC_RB + 2; ++r) {
+            const int ro = r <= lim ? r * rs : lim_off;
 #pragma unroll
-            for (int kw = 0; kw < 3; ++kw) {
-                const int rr = min(r0 + r, DH + 1);
-                xv[r][kw] = *reinterpret_cast<const uint2*>(src + (rr * SW + c + kw) * ss + g * 4);
-            }
+            for (int kw = 0; kw < 3; ++kw) xv[r][kw] = *reinterpret_cast<const uint2*>(sp + ro + kw * ss);
+        }
 #pragma unroll
         for (int o = 0; o < HC_RB; ++o) {
             if (r0 + o >= DH) break;
@@ -239,8 +252,9 @@ __device__ __forceinline__ void hc_pw_units(const T* src, int ss, int NPX, const
     const int l32 = lane & 31, h = lane >> 5;
     const int na = (M + 31) >> 5, nb = (NPX + 31) >> 5;
     hc_barrier();   // src complete
+    const HcDiv dna = hc_div(na, 16);
     for (int u = wv; u < na * nb; u += NWV) {
-        const int bi = u / na, a = u - bi * na;
+        const int bi = hc_q(u, dna), a = u - bi * na;
         const int px = bi * 32 + l32;
         const int pxc = px < NPX ? px : NPX - 1;
         const T* brow = src + pxc * ss + 8 * h;
@@ -337,13 +351,15 @@ __device__ __forceinline__ void hc_body(const HeadClsArgs& A, int li, char* hsm)
     for (int cl = 0; cl < C0; cl += ck) {
         // the padded tile (SX = ck + 8: cpp data chunks + 1 pad chunk per pixel) by LDS-DMA,
         // zeros outside the image = dw1's zero padding
-        const int cpp = ck >> 3, cpx = cpp + 1, total = XH * XW * cpx;
+        constexpr int cpp = (NK1 * 16 < HC_CK ? NK1 * 16 : HC_CK) >> 3, cpx = cpp + 1;
+        const int total = XH * XW * cpx;
         {
             const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+            const HcDiv dxw = hc_div(XW, 16);
             for (int i0 = wv * 64; i0 < total; i0 += HEAD_CLS_THREADS) {
                 const int q = i0 + lane;
                 const int px = q / cpx, c = q - px * cpx;
-                const int r = px / XW, cc = px - r * XW;
+                const int r = hc_q(px, dxw), cc = px - r * XW;
                 const int gh = h0 - 2 + r, gw = w0 - 2 + cc;
                 const bool ok = q < total && c < cpp && (unsigned)gh < (unsigned)H && (unsigned)gw < (unsigned)W;
                 const void* src = ok ? (const void*)(x + (((long long)n * H + gh) * W + gw) * V.ldx + cl + c * 8) : A.zero;
@@ -355,8 +371,9 @@ __device__ __forceinline__ void hc_body(const HeadClsArgs& A, int li, char* hsm)
         if (cl + ck < C0) hc_barrier();   // the next chunk overwrites R1
     }
     // 3. pw1: D1 (R2) -> P1 (R1), zero outside the image (dw2's zero padding)
+    const HcDiv dmw = hc_div(MW, 16), dtw = hc_div(TW, 16);
     auto p1_store = [&](int px, int co, uint2 v) {
-        const int r = px / MW, cc = px - r * MW;
+        const int r = hc_q(px, dmw), cc = px - r * MW;
         const int gh = h0 - 1 + r, gw = w0 - 1 + cc;
         if (!((unsigned)gh < (unsigned)H && (unsigned)gw < (unsigned)W)) v = make_uint2(0, 0);
         *reinterpret_cast<uint2*>(R1 + px * L.SM + co) = v;
@@ -392,7 +409,7 @@ __device__ __forceinline__ void hc_body(const HeadClsArgs& A, int li, char* hsm)
     };
     if (A.io)
         pw3([&](int px, int co, uint2 v) {
-            const int r = px / TW, cc = px - r * TW;
+            const int r = hc_q(px, dtw), cc = px - r * TW;
             const int gh = h0 + r, gw = w0 + cc;
             if ((unsigned)gh < (unsigned)H && (unsigned)gw < (unsigned)W) {
                 T* col = reinterpret_cast<T*>(const_cast<void*>(A.io[1])) +
@@ -404,7 +421,7 @@ __device__ __forceinline__ void hc_body(const HeadClsArgs& A, int li, char* hsm)
         });
     else
         pw3([&](int px, int co, uint2 v) {
-            const int r = px / TW, cc = px - r * TW;
+            const int r = hc_q(px, dtw), cc = px - r * TW;
             const int gh = h0 + r, gw = w0 + cc;
             if ((unsigned)gh < (unsigned)H && (unsigned)gw < (unsigned)W)
                 *reinterpret_cast<uint2*>(y + (((long long)n * H + gh) * W + gw) * V.ldy + co) = v;
