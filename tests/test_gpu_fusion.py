@@ -157,20 +157,54 @@ def test_attention_lds_kernel_equals_per_wave_kernel(gpu, variant, dtype, batch,
     model = make_model(variant)
     x = synth.synth_scenes(batch, size, size, seed=33).to(gpu, dtype)
     ys = []
+    old_full = os.environ.get("YH_ATTN_FULL")
+    os.environ["YH_ATTN_FULL"] = "0"   # the chunked kernel, not the whole-K/V one, where both apply
+    try:
+        for v in ("0", "1"):
+            old = os.environ.get("YH_ATTN_LDS")
+            os.environ["YH_ATTN_LDS"] = v
+            try:
+                eng = _engine(model, dtype, gpu, True)
+                ys.append(eng.forward(x).clone())
+                torch.cuda.synchronize()
+            finally:
+                if old is None:
+                    del os.environ["YH_ATTN_LDS"]
+                else:
+                    os.environ["YH_ATTN_LDS"] = old
+    finally:
+        if old_full is None:
+            del os.environ["YH_ATTN_FULL"]
+        else:
+            os.environ["YH_ATTN_FULL"] = old_full
+    assert torch.isfinite(ys[0].float()).all()
+    assert torch.equal(ys[0], ys[1])
+
+
+@pytest.mark.parametrize("variant,dtype,batch,size", [("n", torch.bfloat16, 4, 640), ("s", torch.float16, 2, 320),
+                                                      ("n", torch.float16, 2, 224), ("m", torch.bfloat16, 2, 480)])
+def test_attention_full_kernel_equals_chunked_kernel_and_pe_add(gpu, variant, dtype, batch, size):
+    """misc.hip psa_attention_full (one workgroup per (image, head), the whole K / V in LDS, the
+    positional term added in the epilogue) is bit-identical to the chunked kernel followed by
+    pe_add (YH_ATTN_FULL=0), including partial key blocks (224: 49 tokens) and several heads
+    (m: 4 heads at 480 -> 225 tokens)."""
+    model = make_model(variant)
+    x = synth.synth_scenes(batch, size, size, seed=34).to(gpu, dtype)
+    ys = []
     for v in ("0", "1"):
-        old = os.environ.get("YH_ATTN_LDS")
-        os.environ["YH_ATTN_LDS"] = v
+        old = os.environ.get("YH_ATTN_FULL")
+        os.environ["YH_ATTN_FULL"] = v
         try:
             eng = _engine(model, dtype, gpu, True)
             ys.append(eng.forward(x).clone())
             torch.cuda.synchronize()
         finally:
             if old is None:
-                del os.environ["YH_ATTN_LDS"]
+                del os.environ["YH_ATTN_FULL"]
             else:
-                os.environ["YH_ATTN_LDS"] = old
+                os.environ["YH_ATTN_FULL"] = old
     assert torch.isfinite(ys[0].float()).all()
-    assert torch.equal(ys[0], ys[1])
+    assert torch.equal(ys[0], ys[1]), (ys[0].float() - ys[1].float()).abs().max().item()
 
 
 @pytest.mark.parametrize("bands", ["1", "2", "3", "5", "7", "20"])

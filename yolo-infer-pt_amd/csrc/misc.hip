@@ -8,6 +8,7 @@
 #include "common.h"
 #include "dtypes.h"
 
+#include <algorithm>
 #include <cstdlib>
 
 namespace yh {
@@ -438,6 +439,119 @@ __global__ __launch_bounds__(64 * AT_NW) void psa_attention_lds(const AttnArgs p
     }
 }
 
+// One workgroup per (image, head) with the head's whole K and V in LDS (maps of up to
+// AF_TMAX tokens: v11 at 640 x 640 has 400): every qkv byte is read once, and pe_add's
+// positional term is added in the epilogue from the V already in LDS, so the attention
+// output is written once (7x, then 4.96x the algorithmic bytes with the
+// chunked kernel and a separate pe_add). Each wave runs psa_attention_mfma's per-16-key-block
+// arithmetic for its 16-query blocks in the same key order, rounds the output as that kernel
+// stores it, then adds pe_b and the 3 x 3 taps in pe_add's order with pe_add's fmaf chain:
+// the result is bit-identical to psa_attention_mfma / psa_attention_lds followed by pe_add.
+constexpr int AF_NW = 16, AF_TMAX = 640;
+__host__ __device__ inline int af_lds_bytes(int T) {
+    const int t16 = (T + 15) & ~15;
+    return t16 * (DK + AT_VS) * 2 + 10 * DH * 4;
+}
+template <typename T>
+__global__ __launch_bounds__(64 * AF_NW) void psa_attention_full(const AttnArgs p) {
+    extern __shared__ __attribute__((aligned(16))) char afs[];
+    const int t16 = (p.T + 15) & ~15;
+    T* klds = reinterpret_cast<T*>(afs);
+    T* vlds = klds + t16 * DK;
+    float* pew = reinterpret_cast<float*>(vlds + t16 * AT_VS);   // [9][DH] of this head, then pe_b
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int qs = gridDim.x / p.heads;   // workgroups per (image, head), splitting the queries
+    const int head = blockIdx.x / qs, split = blockIdx.x - head * qs, n = blockIdx.y;
+    const int g = lane >> 4, li = lane & 15;
+    const int C = p.heads * DH;
+    const T* base = reinterpret_cast<const T*>(p.qkv) + (long long)n * p.T * p.ldq + head * (2 * DK + DH);
+    const uint4 z4 = make_uint4(0, 0, 0, 0);
+    // every token row [k(32) | v(64)] once (zeros past the last token: the per-wave kernel's
+    // missing keys), the head's positional weights and bias
+    for (int i = threadIdx.x; i < t16 * 12; i += 64 * AF_NW) {
+        const int r = i / 12, c = i - r * 12;
+        const uint4 v = r < p.T ? *reinterpret_cast<const uint4*>(base + (long long)r * p.ldq + DK + 8 * c) : z4;
+        if (c < 4) *reinterpret_cast<uint4*>(klds + r * DK + 8 * c) = v;
+        else *reinterpret_cast<uint4*>(vlds + r * AT_VS + 8 * (c - 4)) = v;
+    }
+    for (int i = threadIdx.x; i < 10 * DH; i += 64 * AF_NW)
+        pew[i] = i < 9 * DH ? p.pe_w[(i / DH) * C + head * DH + (i % DH)] : p.pe_b[head * DH + i - 9 * DH];
+    __syncthreads();
+    const int nqb = (p.T + 15) >> 4;
+    for (int qb = split * AF_NW + wave; qb < nqb; qb += qs * AF_NW) {   // wave-uniform
+        const int q = qb * 16 + li;
+        const uint4 qf = q < p.T ? *reinterpret_cast<const uint4*>(base + (long long)q * p.ldq + 8 * g) : z4;
+        f32x4 o[4];
+#pragma unroll
+        for (int t = 0; t < 4; ++t) o[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+        float mrun = -INFINITY, lrun = 0.f;
+        for (int kb = 0; kb < p.T; kb += 16) {
+            const int key = kb + li;
+            const uint4 kf = key < p.T ? *reinterpret_cast<const uint4*>(klds + key * DK + 8 * g) : z4;
+            f32x4 s = f32x4{0.f, 0.f, 0.f, 0.f};
+            Mma<T>::step(s, &kf, &qf);
+            float sv[4], mx = -INFINITY;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                sv[r] = (kb + 4 * g + r < p.T) ? s[r] * p.scale : -INFINITY;
+                mx = fmaxf(mx, sv[r]);
+            }
+            mx = fmaxf(mx, __shfl_xor(mx, 16));
+            mx = fmaxf(mx, __shfl_xor(mx, 32));
+            const float mnew = fmaxf(mrun, mx);
+            const float corr = __expf(mrun - mnew);
+            float ps = 0.f;
+            s16x4 pb;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const float pr = __expf(sv[r] - mnew);
+                pb[r] = __builtin_bit_cast(short, fromf<T>(pr));
+                ps += pr;
+            }
+            ps += __shfl_xor(ps, 16);
+            ps += __shfl_xor(ps, 32);
+            lrun = lrun * corr + ps;
+            mrun = mnew;
+#pragma unroll
+            for (int t = 0; t < 4; ++t) o[t] *= corr;
+            const int kr = kb + 4 * g + (li >> 2);
+#pragma unroll
+            for (int t = 0; t < 4; ++t) {
+                s16x4 a = lds_tr16(vlds + kr * AT_VS + 16 * t + 4 * (li & 3));
+                o[t] = Mma16<T>::step(a, pb, o[t]);
+            }
+        }
+        if (q >= p.T) continue;
+        const float inv = 1.0f / lrun;
+        const int hq = q / p.Ws, wq = q - hq * p.Ws;
+        T* out = reinterpret_cast<T*>(p.out) + ((long long)n * p.T + q) * p.ldo + head * DH;
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+            float acc[4];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) acc[r] = tof(fromf<T>(o[t][r] * inv)) + pew[9 * DH + 16 * t + 4 * g + r];
+#pragma unroll
+            for (int kh = 0; kh < 3; ++kh) {
+                const int hi = hq - 1 + kh;
+                if (hi < 0 || hi >= p.Hs) continue;
+#pragma unroll
+                for (int kw = 0; kw < 3; ++kw) {
+                    const int wi = wq - 1 + kw;
+                    if (wi < 0 || wi >= p.Ws) continue;
+                    const T* vr = vlds + (hi * p.Ws + wi) * AT_VS + 16 * t + 4 * g;
+                    const float* wt = pew + (kh * 3 + kw) * DH + 16 * t + 4 * g;
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) acc[r] = fmaf(wt[r], tof(vr[r]), acc[r]);
+                }
+            }
+            unsigned u[4];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) u[r] = (unsigned short)__builtin_bit_cast(short, fromf<T>(acc[r]));
+            *reinterpret_cast<uint2*>(out + 16 * t + 4 * g) = make_uint2(u[0] | (u[1] << 16), u[2] | (u[3] << 16));
+        }
+    }
+}
+
 // out[:, c] += pe_b[c] + sum_taps pe_w[tap][c] * v[nbr][c]   (c = head*dh + d; v lives in qkv)
 template <typename T>
 __global__ __launch_bounds__(256) void pe_add(const AttnArgs p, int B) {
@@ -479,6 +593,24 @@ int launch_attention_t(const AttnArgs& a, int B, hipStream_t s) {
     if constexpr (sizeof(T) == 2) {
         // YH_ATTN_LDS=0 (read per launch, so per captured graph): the per-wave kernel, which
         // the tests compare bit for bit
+        // YH_ATTN_FULL=0 (read per launch): the chunked kernel + pe_add where the full one applies
+        const char* ef = getenv("YH_ATTN_FULL");
+        if (a.T <= AF_TMAX && a.Ws > 0 && a.Hs * a.Ws == a.T && !(ef && atoi(ef) == 0)) {
+            static bool attr = false;
+            if (!attr) {
+                (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&psa_attention_full<T>),
+                                          hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+                attr = true;
+            }
+            // YH_ATTN_QS: workgroups per (image, head) (each stages the whole K / V; default 2:
+            // at 1 a batch of 32 ran on 64 workgroups, 39 vs 27 us per forward)
+            const char* eq = getenv("YH_ATTN_QS");
+            const int nqb = (a.T + 15) >> 4;
+            const int qs = std::max(1, std::min(eq ? atoi(eq) : 2, (nqb + AF_NW - 1) / AF_NW));
+            hipLaunchKernelGGL((psa_attention_full<T>), dim3((unsigned)(a.heads * qs), (unsigned)B), dim3(64 * AF_NW),
+                               af_lds_bytes(a.T), s, a);
+            return (int)hipGetLastError();
+        }
         const char* e = getenv("YH_ATTN_LDS");
         if (e && atoi(e) == 0) {
             const dim3 g((a.T + 63) / 64, a.heads, B);
