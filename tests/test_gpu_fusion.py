@@ -207,6 +207,32 @@ def test_attention_full_kernel_equals_chunked_kernel_and_pe_add(gpu, variant, dt
     assert torch.equal(ys[0], ys[1]), (ys[0].float() - ys[1].float()).abs().max().item()
 
 
+@pytest.mark.parametrize("variant,dtype,batch,size", [("n", torch.bfloat16, 4, 640), ("s", torch.float16, 2, 320),
+                                                      ("x", torch.bfloat16, 1, 1280), ("n", torch.float16, 2, 224)])
+def test_sppf_kernel_equals_three_maxpools(gpu, variant, dtype, batch, size):
+    """misc.hip sppf_fused (CPW 8-channel chunks of one image per workgroup, chosen by the LDS:
+    8 at 20x20, 2 at 40x40) and with one chunk per workgroup (YH_SPPF_CPW=1) are bit-identical
+    to three maxpool5 launches (YH_SPPF_FUSED=0). Both switches are read at launch."""
+    model = make_model(variant)
+    x = synth.synth_scenes(batch, size, size, seed=35).to(gpu, dtype)
+    ys = []
+    for env in ({"YH_SPPF_FUSED": "0"}, {"YH_SPPF_CPW": "1"}, {}):
+        old = {k: os.environ.get(k) for k in ("YH_SPPF_FUSED", "YH_SPPF_CPW")}
+        os.environ.update(env)
+        try:
+            eng = _engine(model, dtype, gpu, True)
+            ys.append(eng.forward(x).clone())
+            torch.cuda.synchronize()
+        finally:
+            for k, v in old.items():
+                if v is None:
+                    os.environ.pop(k, None)
+                else:
+                    os.environ[k] = v
+    assert torch.isfinite(ys[0].float()).all()
+    assert torch.equal(ys[0], ys[1]) and torch.equal(ys[0], ys[2])
+
+
 @pytest.mark.parametrize("bands", ["1", "2", "3", "5", "7", "20"])
 def test_c3k_row_bands_equal_per_layer_launches(gpu, bands):
     """c3k.hip row bands: each image's block is split over `bands` workgroups that recompute the

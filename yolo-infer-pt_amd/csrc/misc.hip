@@ -52,43 +52,61 @@ __global__ __launch_bounds__(256) void maxpool5(const T* src, T* dst, int ldc, i
     st_chunk(dst + (long long)m * ldc + cc * 8, f_to_chunk<T>(mx));
 }
 
-// All three pools in one launch: a workgroup owns one (image, 8-channel chunk)
-// plane, staged in LDS once; y1 = mp(x), y2 = mp(y1), y3 = mp(y2) ping-pong
-// between two LDS planes and each is stored to its concat slice. Max is exact,
-// so this is bit-identical to three maxpool5 launches (which it replaces
-// whenever two planes fit in LDS: H * W <= SPPF_MAX_PX).
-constexpr int SPPF_MAX_PX = 4096;
+// All three pools in one launch: a workgroup owns CPW consecutive 8-channel chunks of one
+// image (CPW * 16 contiguous bytes of every pixel per load and store), staged in LDS once;
+// y1 = mp(x), y2 = mp(y1), y3 = mp(y2), each as a 1 x 5 row max into a scratch plane and a
+// 5 x 1 column max of that (10 LDS reads per output instead of 25), stored to its concat
+// slice. Max is exact and associative, so this is bit-identical to three maxpool5 launches
+// (which it replaces whenever three planes fit in LDS).
+// running max of 8 channels from -inf (fmaxf: NaN taps are skipped, as in maxpool5)
 template <typename T>
-__global__ __launch_bounds__(256) void sppf_fused(const PoolArgs a) {
+__device__ __forceinline__ void sppf_acc(float (&mx)[8], uint4 v) {
+    Chunk<T> c;
+    c.v[0] = v;
+    float f[8];
+    chunk_to_f(c, f);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) mx[e] = fmaxf(mx[e], f[e]);
+}
+template <typename T>
+__global__ __launch_bounds__(256) void sppf_fused(const PoolArgs a, int cpw) {
     extern __shared__ __attribute__((aligned(16))) uint4 pln[];
-    const int cpp = a.C / 8;
-    const int n = blockIdx.x / cpp, cc = blockIdx.x - n * cpp;
-    const int HW = a.H * a.W;
+    const int cpp = a.C / 8, ng = cpp / cpw;
+    const int n = blockIdx.x / ng, cc = (blockIdx.x - n * ng) * cpw;
+    const int HW = a.H * a.W, NI = HW * cpw;
     T* img = reinterpret_cast<T*>(a.buf) + (long long)n * HW * a.ldc + cc * 8;
-    uint4* p0 = pln;
-    uint4* p1 = pln + HW;
-    for (int px = threadIdx.x; px < HW; px += 256) p0[px] = *reinterpret_cast<const uint4*>(img + (long long)px * a.ldc);
+    uint4* p0 = pln;         // pool input / output planes (ping-pong)
+    uint4* p1 = pln + NI;
+    uint4* rm = pln + 2 * NI;   // row maxima
+    // item i = (pixel i / cpw, chunk i % cpw): consecutive threads, consecutive 16 B of a pixel
+    for (int i = threadIdx.x; i < NI; i += 256) {
+        const int px = i / cpw, c = i - px * cpw;
+        p0[i] = *reinterpret_cast<const uint4*>(img + (long long)px * a.ldc + 8 * c);
+    }
     __syncthreads();
-    for (int i = 0; i < 3; ++i) {
-        const uint4* src = (i & 1) ? p1 : p0;
-        uint4* dst = (i & 1) ? p0 : p1;
-        for (int px = threadIdx.x; px < HW; px += 256) {
+    for (int it = 0; it < 3; ++it) {
+        const uint4* src = (it & 1) ? p1 : p0;
+        uint4* dst = (it & 1) ? p0 : p1;
+        for (int i = threadIdx.x; i < NI; i += 256) {
+            const int px = i / cpw, c = i - px * cpw;
             const int h = px / a.W, w = px - h * a.W;
             float mx[8];
 #pragma unroll
             for (int e = 0; e < 8; ++e) mx[e] = -INFINITY;
-            for (int hi = max(h - 2, 0); hi <= min(h + 2, a.H - 1); ++hi)
-                for (int wi = max(w - 2, 0); wi <= min(w + 2, a.W - 1); ++wi) {
-                    Chunk<T> c;
-                    c.v[0] = src[hi * a.W + wi];
-                    float f[8];
-                    chunk_to_f(c, f);
+            for (int wi = max(w - 2, 0); wi <= min(w + 2, a.W - 1); ++wi) sppf_acc<T>(mx, src[(h * a.W + wi) * cpw + c]);
+            rm[i] = f_to_chunk<T>(mx).v[0];
+        }
+        __syncthreads();
+        for (int i = threadIdx.x; i < NI; i += 256) {
+            const int px = i / cpw, c = i - px * cpw;
+            const int h = px / a.W, w = px - h * a.W;
+            float mx[8];
 #pragma unroll
-                    for (int e = 0; e < 8; ++e) mx[e] = fmaxf(mx[e], f[e]);
-                }
-            const Chunk<T> o = f_to_chunk<T>(mx);
-            dst[px] = o.v[0];
-            *reinterpret_cast<uint4*>(img + (long long)px * a.ldc + (i + 1) * a.C) = o.v[0];
+            for (int e = 0; e < 8; ++e) mx[e] = -INFINITY;
+            for (int hi = max(h - 2, 0); hi <= min(h + 2, a.H - 1); ++hi) sppf_acc<T>(mx, rm[(hi * a.W + w) * cpw + c]);
+            const uint4 m = f_to_chunk<T>(mx).v[0];
+            dst[i] = m;
+            *reinterpret_cast<uint4*>(img + (long long)px * a.ldc + (it + 1) * a.C + 8 * c) = m;
         }
         __syncthreads();
     }
@@ -99,15 +117,23 @@ int launch_sppf_t(const PoolArgs& a, hipStream_t s) {
     T* b = reinterpret_cast<T*>(a.buf);
     const int M = a.B * a.H * a.W;
     if constexpr (sizeof(T) == 2) {
-        if (a.H * a.W <= SPPF_MAX_PX && a.C % 8 == 0) {
+        // YH_SPPF_FUSED=0 (read per launch): the three maxpool5 launches (the tests compare both)
+        const char* ef = getenv("YH_SPPF_FUSED");
+        if (3 * a.H * a.W * 16 <= 160 * 1024 && a.C % 8 == 0 && !(ef && atoi(ef) == 0)) {
             static bool attr_set = false;
             if (!attr_set) {
                 (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&sppf_fused<T>),
                                           hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
                 attr_set = true;
             }
-            hipLaunchKernelGGL((sppf_fused<T>), dim3((unsigned)(a.B * (a.C / 8))), dim3(256),
-                               2 * a.H * a.W * (int)sizeof(uint4), s, a);
+            // chunks per workgroup: the most of 8 / 4 / 2 / 1 that divides the channels and whose
+            // two planes fit the LDS (YH_SPPF_CPW: at most that many)
+            const char* e = getenv("YH_SPPF_CPW");
+            int cpw = e ? std::max(1, atoi(e)) : 2;
+            while (cpw > 1 && ((a.C / 8) % cpw || 3 * a.H * a.W * cpw * 16 > 160 * 1024))
+                cpw >>= 1;
+            hipLaunchKernelGGL((sppf_fused<T>), dim3((unsigned)(a.B * (a.C / 8 / cpw))), dim3(256),
+                               3 * a.H * a.W * cpw * (int)sizeof(uint4), s, a, cpw);
             return (int)hipGetLastError();
         }
     }
