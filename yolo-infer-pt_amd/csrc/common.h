@@ -222,7 +222,7 @@ struct CspArgs {
     const void* zero;                // >= 16 zero bytes
 };
 #ifndef YH_CSP_THREADS
-#define YH_CSP_THREADS 512
+#define YH_CSP_THREADS 1024
 #endif
 constexpr int CSP_THREADS = YH_CSP_THREADS;
 // bytes of the packed parameter image (weight fragments in MFMA lane order + biases)

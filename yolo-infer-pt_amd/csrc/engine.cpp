@@ -603,12 +603,27 @@ struct Net {
     // tail mode even where the whole block fits one launch (Options::csp_tail, tests)
     bool tail_first() const { return opt.csp_tail; }
     static bool csp_tile(int ni, int nc, int no, int H, int W, int& TH, int& TW) {
-        static const int cand[][2] = {{8, 16}, {8, 8}, {4, 16}, {4, 8}, {2, 8}, {2, 4}};
-        // the largest tile of >= 64 pixels that leaves room for a second workgroup per CU,
-        // else the largest that fits (measured: net.p3.1 at 2x4 tiles, two per CU, 263 us
-        // against 68 us at 8x16, one per CU)
+        // YH_CSP_TILE=<TH>x<TW> (experiments): that tile first where it fits one workgroup
+        if (const char* e = getenv("YH_CSP_TILE")) {
+            int th = 0, tw = 0;
+            if (sscanf(e, "%dx%d", &th, &tw) == 2 && th > 0 && tw > 0 && th <= H && tw <= W &&
+                csp_lds(th, tw, ni, nc, no) > 0) {
+                TH = th;
+                TW = tw;
+                return true;
+            }
+        }
+        // 16-wave workgroups (one per CU): the largest tile that fits (8 x 32 / 16 x 16 against
+        // 8-wave 8 x 16 pairs: bench +2.5 %, net.p3.1 65 -> 62 us, fpn.h2.tail 40 -> 37 us);
+        // 8-wave ones: the largest tile of >= 64 pixels that leaves room for a second workgroup
+        // per CU, else the largest that fits (measured: net.p3.1 at 2x4 tiles, two per CU,
+        // 263 us against 68 us at 8x16, one per CU)
+        static const int cand[][2] = {{8, 32}, {16, 16}, {8, 16}, {8, 8}, {4, 16}, {4, 8}, {2, 8}, {2, 4}};
+        const bool wide = CSP_THREADS >= 1024;
         for (int lim : {80 * 1024, 160 * 1024})
             for (auto& c : cand) {
+                if (wide && lim == 80 * 1024) break;
+                if (!wide && c[0] * c[1] > 128) continue;
                 if (c[0] > H || c[1] > W || (lim == 80 * 1024 && c[0] * c[1] < 64)) continue;
                 const int b = csp_lds(c[0], c[1], ni, nc, no);
                 if (b > 0 && b <= lim) {
@@ -1359,7 +1374,13 @@ struct Net {
                 a.zero = zero_dev;
                 if (!num_cus) HIPCHECK(hipDeviceGetAttribute(&num_cus, hipDeviceAttributeMultiprocessorCount, device));
                 // two workgroups per CU when the LDS allows (measured: net.p2.1 138 -> 103 us at b32)
-                rc = launch_csp(dtype, a, std::min(a.ntiles, 2 * num_cus), s);
+                {
+                    // persistent workgroups: as many as are resident at once (two per CU where the
+                    // LDS allows)
+                    const int lds = csp_lds(a.TH, a.TW, a.ni, a.nc, a.no);
+                    const int per_cu = CSP_THREADS < 1024 && lds > 0 && lds <= 80 * 1024 ? 2 : 1;
+                    rc = launch_csp(dtype, a, std::min(a.ntiles, per_cu * num_cus), s);
+                }
                 break;
             }
             case OP_C3K: {
