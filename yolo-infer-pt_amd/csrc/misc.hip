@@ -479,15 +479,19 @@ __host__ __device__ inline int af_lds_bytes(int T) {
     return t16 * (DK + AT_VS) * 2 + 10 * DH * 4;
 }
 template <typename T>
-__global__ __launch_bounds__(64 * AF_NW) void psa_attention_full(const AttnArgs p) {
+__global__ __launch_bounds__(64 * AF_NW) void psa_attention_full(const AttnArgs p, int B) {
     extern __shared__ __attribute__((aligned(16))) char afs[];
     const int t16 = (p.T + 15) & ~15;
     T* klds = reinterpret_cast<T*>(afs);
     T* vlds = klds + t16 * DK;
     float* pew = reinterpret_cast<float*>(vlds + t16 * AT_VS);   // [9][DH] of this head, then pe_b
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const int qs = gridDim.x / p.heads;   // workgroups per (image, head), splitting the queries
-    const int head = blockIdx.x / qs, split = blockIdx.x - head * qs, n = blockIdx.y;
+    // block id = (image, head) pair + pairs x split: the workgroups of one pair are 8 x k ids
+    // apart when the pair count is a multiple of 8, i.e. on the same XCD (one L2), so the second
+    // one's K / V reads meet the first one's in L2
+    const int np = p.heads * B, qs = gridDim.x / np;   // workgroups per (image, head), splitting the queries
+    const int split = blockIdx.x / np, pair = blockIdx.x - split * np;
+    const int n = pair / p.heads, head = pair - n * p.heads;
     const int g = lane >> 4, li = lane & 15;
     const int C = p.heads * DH;
     const T* base = reinterpret_cast<const T*>(p.qkv) + (long long)n * p.T * p.ldq + head * (2 * DK + DH);
@@ -633,8 +637,8 @@ int launch_attention_t(const AttnArgs& a, int B, hipStream_t s) {
             const char* eq = getenv("YH_ATTN_QS");
             const int nqb = (a.T + 15) >> 4;
             const int qs = std::max(1, std::min(eq ? atoi(eq) : 2, (nqb + AF_NW - 1) / AF_NW));
-            hipLaunchKernelGGL((psa_attention_full<T>), dim3((unsigned)(a.heads * qs), (unsigned)B), dim3(64 * AF_NW),
-                               af_lds_bytes(a.T), s, a);
+            hipLaunchKernelGGL((psa_attention_full<T>), dim3((unsigned)(a.heads * B * qs)), dim3(64 * AF_NW),
+                               af_lds_bytes(a.T), s, a, B);
             return (int)hipGetLastError();
         }
         const char* e = getenv("YH_ATTN_LDS");
