@@ -214,7 +214,9 @@ __global__ __launch_bounds__(CK_THREADS, 1) void c3k_fused(const C3kArgs A) {
     typedef __attribute__((address_space(3))) char* lds_c;
     const unsigned lds0 = (unsigned)(size_t)(lds_c)sm;
     // band rows [r0, r1) of image n; LDS region rows [ra0, ra1) (the band + its 4-row halo)
-    const int n = blockIdx.x / A.bands, band = blockIdx.x - n * A.bands;
+    // XCD-aware: the bands of one image (whose halo rows overlap) on one XCD, i.e. one L2
+    const int lb = xcd_remap(blockIdx.x, gridDim.x);
+    const int n = lb / A.bands, band = lb - n * A.bands;
     const int RB = (A.H + A.bands - 1) / A.bands;
     const int r0 = band * RB, r1 = min(A.H, r0 + RB);
     const int ra0 = max(0, r0 - 4), ra1 = min(A.H, r1 + 4);

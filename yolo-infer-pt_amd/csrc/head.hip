@@ -299,7 +299,8 @@ __device__ __forceinline__ void hc_pw_units(const T* src, int ss, int NPX, const
 template <typename T, int NK1, int NAP1, int NK2>
 __device__ __forceinline__ void hc_body(const HeadClsArgs& A, int li, char* hsm) {
     const HeadClsLevel& V = A.lv[li];
-    const int wl = blockIdx.x - V.wg0;
+    // XCD-aware within the level: neighbouring tiles (overlapping halos) on one XCD / L2
+    const int wl = xcd_remap((int)blockIdx.x - V.wg0, A.B * V.tiles);
     const int n = wl / V.tiles, tix = wl - n * V.tiles;
     const int ty = tix / V.ntw, tx = tix - ty * V.ntw;
     const int TH = V.TH, TW = V.TW, H = V.H, W = V.W;
