@@ -210,9 +210,11 @@ __global__ __launch_bounds__(CSP_THREADS) void csp_fused(const CspArgs A) {
             cs_glds(src, LD + i0 * 16);
         }
     };
-    if ((int)blockIdx.x < A.ntiles) load_x(blockIdx.x);
+    // XCD-aware: the workgroups of one XCD take neighbouring tiles (overlapping halos, one L2)
+    const int t0 = xcd_remap(blockIdx.x, gridDim.x);
+    if (t0 < A.ntiles) load_x(t0);
 
-    for (int t = blockIdx.x; t < A.ntiles; t += gridDim.x) {
+    for (int t = t0; t < A.ntiles; t += gridDim.x) {
         const int n = t / A.tiles, tix = t - n * A.tiles;
         const int ty = tix / A.ntw, tx = tix - ty * A.ntw;
         const int h0 = ty * TH, w0 = tx * TW;
