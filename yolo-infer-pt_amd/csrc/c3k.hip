@@ -195,7 +195,11 @@ __host__ __device__ inline int ck_tt_bytes(int hh, int rpx) {
     return rpx * 2 * hh > w12 ? rpx * 2 * hh : w12;
 }
 
-template <typename T, int HH>
+// SPLIT (h = 64, regions whose phases B..F fit 8 pixel tiles): waves w and w + 8 take the same
+// pixel tile and the two 32-cout tiles of each 3x3 conv (a step multiplies two ring items, one
+// per wave group; conv2's output waits in LDS for phase F): every wave has a tile in every
+// phase instead of half of them, and the number of steps halves. Same per-tile arithmetic.
+template <typename T, int HH, bool SPLIT>
 __global__ __launch_bounds__(CK_THREADS, 1) void c3k_fused(const C3kArgs A) {
     constexpr CkLayout L = ck_layout<HH>();
     constexpr int PX = 2 * HH;                       // LDS bytes per pixel of C1 / T
@@ -210,6 +214,9 @@ __global__ __launch_bounds__(CK_THREADS, 1) void c3k_fused(const C3kArgs A) {
     constexpr int W3 = NTO * NK1 * 1024;             // conv3's weight bytes
     constexpr int TPG = 16 / NK1;                    // conv3 tiles per ring item (16 KB of it)
     constexpr int NITEMS = NHS + (NTO + TPG - 1) / TPG;
+    constexpr int NS = SPLIT ? 2 : 1;                // ring items per step (one per wave group)
+    constexpr int NSTEP = (NITEMS + NS - 1) / NS;
+    static_assert(!SPLIT || (NT3 == 2 && NHS % 2 == 0 && NITEMS - NHS == 2), "two wave groups");
     extern __shared__ __attribute__((aligned(1024))) char sm[];
     typedef __attribute__((address_space(3))) char* lds_c;
     const unsigned lds0 = (unsigned)(size_t)(lds_c)sm;
@@ -225,7 +232,8 @@ __global__ __launch_bounds__(CK_THREADS, 1) void c3k_fused(const C3kArgs A) {
     const int NB = A.nbuf;                           // ring buffers (2 .. CK_MAXNB)
     char* C1 = sm;                                   // [RPX][HH] (swizzled chunks)
     char* TT = sm + RPX * PX;                        // [RPX][HH]; conv1 / conv2's weights before B
-    const int wb_off = RPX * PX + ck_tt_bytes(HH, RPX);
+    char* C2 = TT + ck_tt_bytes(HH, RPX);            // SPLIT: [RB W][HH], conv2(x) of the band's pixels
+    const int wb_off = (int)(C2 - sm) + (SPLIT ? RB * A.W * PX : 0);
     char* WB = sm + wb_off;                          // the ring
     char* ZR = WB + NB * CK_WBH;                     // 128 zero bytes (out-of-image taps)
     const float* BI = reinterpret_cast<const float*>(ZR + 128);   // every bias (32 HH bytes)
@@ -248,6 +256,9 @@ __global__ __launch_bounds__(CK_THREADS, 1) void c3k_fused(const C3kArgs A) {
         if (i >= NHS) {
             src = L.w3 + (i - NHS) * 16 * 1024;
             np = min(16, (W3 - (i - NHS) * 16 * 1024) / 1024);
+        } else if (SPLIT) {   // item order (conv, half, tile): a step's two items are one conv's two tiles
+            const int cv = i / (NT3 * HALVES), rem = i - cv * NT3 * HALVES, half = rem / NT3, t = rem - half * NT3;
+            src = L.wr + ((cv * NT3 + t) * HALVES + half) * CK_WBH;
         }
         const unsigned dst = lds0 + (unsigned)(wb_off + (i % NB) * CK_WBH);
 #pragma unroll
@@ -265,13 +276,19 @@ __global__ __launch_bounds__(CK_THREADS, 1) void c3k_fused(const C3kArgs A) {
     // the wave's pixel tile: 32 consecutive region pixels (clamped; only p < NRP is written).
     // Phases B..F only reach the first 16 tiles (the launcher's bands guarantee it); region
     // pixels past them (bottom halo rows of wide bands) get C1 from extra phase-A tiles.
-    const int p = wv * 32 + l32;
-    const bool own = wv * 32 < NRP;                  // wave-uniform: the wave has a tile
+    // phase A: tile wv (conv1 of all 16 tiles); phases B..F: tile bt = wv (SPLIT: wv % 8) and,
+    // with SPLIT, the cout tile / ring item tg = wv / 8
+    const int pa = wv * 32 + l32;
+    const bool owna = wv * 32 < NRP, pva = pa < NRP;
+    const int bt = SPLIT ? (wv & 7) : wv, tg = SPLIT ? (wv >> 3) : 0;
+    const int p = bt * 32 + l32;
+    const bool own = bt * 32 < NRP;                  // wave-uniform: the wave has a tile
     const bool pv = p < NRP;
     const int pc = pv ? p : NRP - 1;
     const int py = ra0 + pc / A.W, px = pc - (py - ra0) * A.W;   // image row / column
+    const int bofs = (r0 - ra0) * A.W, nbp = (r1 - r0) * A.W;   // band pixels in the region
     // rows of the wave's tile (wave-uniform): a phase runs the tile iff it meets the phase's rows
-    const int ty0 = ra0 + (wv * 32) / A.W, ty1 = ra0 + (min(wv * 32 + 31, NRP - 1)) / A.W;
+    const int ty0 = ra0 + (bt * 32) / A.W, ty1 = ra0 + (min(bt * 32 + 31, NRP - 1)) / A.W;
     auto live = [&](int lo, int hi) { return own && ty1 >= lo && ty0 < hi; };
     auto xrow = [&](int q) {
         const int qy = ra0 + q / A.W, qx = q - (qy - ra0) * A.W;
@@ -279,12 +296,12 @@ __global__ __launch_bounds__(CK_THREADS, 1) void c3k_fused(const C3kArgs A) {
     };
     uint4 xb[NK1];
     {
-        const T* xp = xrow(pc);
+        const T* xp = xrow(pva ? pa : NRP - 1);
 #pragma unroll
         for (int kb = 0; kb < NK1; ++kb) xb[kb] = *reinterpret_cast<const uint4*>(xp + 16 * kb);
     }
-    for (int i = 0; i < NB - 1; ++i) issue(i);
-    if (wv < CK_IW) ck_wait_items(min(NB - 1, NITEMS));   // all but the ring items
+    for (int i = 0; i < NB - NS; ++i) issue(i);
+    if (wv < CK_IW) ck_wait_items(min(NB - NS, NITEMS));   // all but the ring items
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     ck_barrier();
     CK_STAMP(1);
@@ -307,23 +324,32 @@ __global__ __launch_bounds__(CK_THREADS, 1) void c3k_fused(const C3kArgs A) {
             }
         }
     };
-    if (own) {
-        const char* w2 = TT + W12;
-        const float* b2 = BI + (L.b2 - L.b1) / 4;
+    if (owna) {
+        // SPLIT: only tiles that meet the band, conv2's output to C2 (wave-uniform)
+        if (!SPLIT || (wv * 32 + 31 >= bofs && wv * 32 < bofs + nbp)) {
+            const char* w2 = TT + W12;
+            const float* b2 = BI + (L.b2 - L.b1) / 4;
+            const int bp = pa - bofs;
+            const bool bv = pva && bp >= 0 && bp < nbp;
 #pragma unroll
-        for (int t = 0; t < NT3; ++t) {
-            acc = ck_1x1<T, NK1>(w2 + t * NK1 * 1024, lane, xb);
+            for (int t = 0; t < NT3; ++t) {
+                acc = ck_1x1<T, NK1>(w2 + t * NK1 * 1024, lane, xb);
 #pragma unroll
-            for (int jj = 0; jj < 2; ++jj) {
-                const float* bj = b2 + 32 * t + 16 * jj + 8 * h;
-                unsigned w[4];
+                for (int jj = 0; jj < 2; ++jj) {
+                    const float* bj = b2 + 32 * t + 16 * jj + 8 * h;
+                    unsigned w[4];
 #pragma unroll
-                for (int e = 0; e < 8; e += 2)
-                    w[e >> 1] = ck_pack2<T>(silu<T>(acc[8 * jj + e] + bj[e]), silu<T>(acc[8 * jj + e + 1] + bj[e + 1]));
-                bf[NCB + 2 * t + jj] = make_uint4(w[0], w[1], w[2], w[3]);
+                    for (int e = 0; e < 8; e += 2)
+                        w[e >> 1] = ck_pack2<T>(silu<T>(acc[8 * jj + e] + bj[e]), silu<T>(acc[8 * jj + e + 1] + bj[e + 1]));
+                    if (SPLIT) {
+                        if (bv) *reinterpret_cast<uint4*>(C2 + ck_off<HH>(bp, 4 * t + 2 * jj + h)) = make_uint4(w[0], w[1], w[2], w[3]);
+                    } else {
+                        bf[NCB + 2 * t + jj] = make_uint4(w[0], w[1], w[2], w[3]);
+                    }
+                }
             }
         }
-        conv1_tile(p, pv);
+        conv1_tile(pa, pva);
     }
     for (int q0 = wv * 32 + 32 * CK_NW; q0 < NRP; q0 += 32 * CK_NW) {   // wave-uniform
         const int q = q0 + l32;
@@ -358,16 +384,28 @@ __global__ __launch_bounds__(CK_THREADS, 1) void c3k_fused(const C3kArgs A) {
     //      buffer i % NB; items i + 1 .. i + NB - 2 are in flight while it is multiplied, and
     //      item i + NB - 1 is issued into the buffer item i - 1 used.
 #pragma unroll 1
-    for (int i = 0; i < NITEMS; ++i) {
-        if (wv < CK_IW) ck_wait_items(min(NB - 2, NITEMS - 1 - i));   // this wave's pieces of item i
-        ck_barrier();   // ... and everyone's; item i - 1's buffer and the previous phase are done
-        CK_STAMP(3 + i);
-        issue(i + NB - 1);
+    for (int j = 0; j < NSTEP; ++j) {
+        const int i0 = j * NS;
+        // this wave's pieces of the step's items landed (items issued so far: min(i0 + NB - NS,
+        // NITEMS); the ones after the step's may stay in flight)
+        if (wv < CK_IW) ck_wait_items(min(i0 + NB - NS, NITEMS) - min(i0 + NS, NITEMS));
+        ck_barrier();   // ... and everyone's; step j - 1's buffers and the previous phase are done
+        CK_STAMP(3 + j);
+#pragma unroll
+        for (int k = 0; k < NS; ++k) issue(i0 + NB - NS + k);
+        const int i = i0 + tg;                       // this wave's item
         const char* wb = WB + (i % NB) * CK_WBH;
-        if (i >= NHS) {
+        if (i0 >= NHS) {
             // ---- F
-            if (!fl) continue;
-            if (i == NHS) {
+            if (!fl || i >= NITEMS) continue;
+            if (SPLIT) {
+                const int bpc = min(max(pc - bofs, 0), nbp - 1);
+#pragma unroll
+                for (int kb = 0; kb < NCB; ++kb) {
+                    bf[kb] = *reinterpret_cast<const uint4*>(C1 + ck_off<HH>(pc, 2 * kb + h));
+                    bf[NCB + kb] = *reinterpret_cast<const uint4*>(C2 + ck_off<HH>(bpc, 2 * kb + h));
+                }
+            } else if (i == NHS) {
 #pragma unroll
                 for (int kb = 0; kb < NCB; ++kb) bf[kb] = *reinterpret_cast<const uint4*>(C1 + ck_off<HH>(pc, 2 * kb + h));
             }
@@ -388,7 +426,16 @@ __global__ __launch_bounds__(CK_THREADS, 1) void c3k_fused(const C3kArgs A) {
             }
             continue;
         }
-        const int cv = i / (NT3 * HALVES), t = (i / HALVES) % NT3, half = i % HALVES;
+        int cv, t, half;
+        if (SPLIT) {
+            cv = i0 / (NT3 * HALVES);
+            half = (i0 - cv * NT3 * HALVES) / NT3;
+            t = tg;
+        } else {
+            cv = i / (NT3 * HALVES);
+            t = (i / HALVES) % NT3;
+            half = i % HALVES;
+        }
         char* src = (cv & 1) ? TT : C1;
         char* dst = (cv & 1) ? C1 : TT;
         // rows this conv must produce: the band + (3 - cv) halo rows (what conv cv + 1 reads)
@@ -440,12 +487,12 @@ __global__ __launch_bounds__(CK_THREADS, 1) void c3k_fused(const C3kArgs A) {
             *reinterpret_cast<uint4*>(dst + o1) = make_uint4(w[4], w[5], w[6], w[7]);
         }
     }
-    CK_STAMP(3 + NITEMS);
+    CK_STAMP(3 + NSTEP);
 }
 
 // LDS bytes of a workgroup with region images of rpx pixels and nb ring buffers
-static long long ck_lds_px(int hh, long long rpx, int nb) {
-    return rpx * 2 * hh + ck_tt_bytes(hh, (int)rpx) + (long long)nb * CK_WBH + 128 + 32 * hh;
+static long long ck_lds_px(int hh, long long rpx, int nb, long long bpx = 0) {
+    return rpx * 2 * hh + ck_tt_bytes(hh, (int)rpx) + bpx * 2 * hh + (long long)nb * CK_WBH + 128 + 32 * hh;
 }
 
 // pixels from a band region's first row to the last row phases B..F use (the band + 3 halo
@@ -471,22 +518,27 @@ template <typename T, int HH>
 int launch_c3k_t(const C3kArgs& a0, hipStream_t s) {
     C3kArgs a = a0;
     a.bands = c3k_bands(a.B, a.H, a.W, HH);
-    const int rpx = ck_region_px(a.H, a.W, a.bands);
-    // as many ring buffers as the LDS holds (YH_C3K_NB: fewer)
+    const int rpx = ck_region_px(a.H, a.W, a.bands), bpx = (a.H + a.bands - 1) / a.bands * a.W;
+    // SPLIT where phases B..F fit 8 tiles and the ring keeps >= 4 buffers beside conv2's
+    // band (YH_C3K_SPLIT=0: never); as many ring buffers as the LDS holds (YH_C3K_NB: fewer)
+    static const bool split_ok = [] { const char* e = getenv("YH_C3K_SPLIT"); return !e || atoi(e) != 0; }();
+    const bool split = HH == 64 && split_ok && ck_live_px(a.H, a.W, a.bands) <= 32 * 8 &&
+                       ck_lds_px(HH, rpx, 4, bpx) <= 160 * 1024;
+    const long long bp = split ? bpx : 0;
     a.nbuf = 2;
-    while (a.nbuf < CK_MAXNB && ck_lds_px(HH, rpx, a.nbuf + 1) <= 160 * 1024) ++a.nbuf;
-    if (const char* e = getenv("YH_C3K_NB")) a.nbuf = std::max(2, std::min(a.nbuf, atoi(e)));
-    const long long lds = ck_lds_px(HH, rpx, a.nbuf);
+    while (a.nbuf < CK_MAXNB && ck_lds_px(HH, rpx, a.nbuf + 1, bp) <= 160 * 1024) ++a.nbuf;
+    if (const char* e = getenv("YH_C3K_NB")) a.nbuf = std::max(split ? 4 : 2, std::min(a.nbuf, atoi(e)));
+    const long long lds = ck_lds_px(HH, rpx, a.nbuf, bp);
     if (c3k_lds(a.H, a.W, HH) == 0 || ck_live_px(a.H, a.W, a.bands) > 32 * CK_NW || rpx > 2 * 32 * CK_NW ||
         lds > 160 * 1024 || a.B < 1 || a.ldx % 8 || a.ldy % 8)
         return (int)hipErrorInvalidValue;
-    static bool attr = false;
-    if (!attr) {
-        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&c3k_fused<T, HH>), hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  160 * 1024);
-        attr = true;
+    auto k = split ? &c3k_fused<T, HH, HH == 64> : &c3k_fused<T, HH, false>;
+    static bool attr[2] = {false, false};
+    if (!attr[split]) {
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        attr[split] = true;
     }
-    hipLaunchKernelGGL((c3k_fused<T, HH>), dim3((unsigned)(a.B * a.bands)), dim3(CK_THREADS), (int)lds, s, a);
+    hipLaunchKernelGGL(k, dim3((unsigned)(a.B * a.bands)), dim3(CK_THREADS), (int)lds, s, a);
     return (int)hipGetLastError();
 }
 
