@@ -390,8 +390,13 @@ __global__ __launch_bounds__(64 * AT_NW) void psa_attention_lds(const AttnArgs p
     __shared__ __attribute__((aligned(16))) T klds[AT_KC * DK];
     __shared__ __attribute__((aligned(16))) T vlds[AT_KC * AT_VS];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const int q0 = (blockIdx.x * AT_NW + wave) * 16;
-    const int head = blockIdx.y, n = blockIdx.z;
+    // 1-D grid, block id = (image, head) pair + pairs x query group: the query groups of one
+    // pair are 8 x k ids apart (pair count a multiple of 8), i.e. on one XCD / L2, where their
+    // K / V reads meet
+    const int np = (int)gridDim.x / ((p.T + 16 * AT_NW - 1) / (16 * AT_NW));
+    const int qg = blockIdx.x / np, pair = blockIdx.x - qg * np;
+    const int n = pair / p.heads, head = pair - n * p.heads;
+    const int q0 = (qg * AT_NW + wave) * 16;
     const int g = lane >> 4, li = lane & 15;
     const T* base = reinterpret_cast<const T*>(p.qkv) + (long long)n * p.T * p.ldq + head * (2 * DK + DH);
     const uint4 z4 = make_uint4(0, 0, 0, 0);
@@ -646,8 +651,8 @@ int launch_attention_t(const AttnArgs& a, int B, hipStream_t s) {
             const dim3 g((a.T + 63) / 64, a.heads, B);
             hipLaunchKernelGGL((psa_attention_mfma<T>), g, dim3(256), 0, s, a);
         } else {
-            const dim3 g((a.T + 16 * AT_NW - 1) / (16 * AT_NW), a.heads, B);
-            hipLaunchKernelGGL((psa_attention_lds<T>), g, dim3(64 * AT_NW), 0, s, a);
+            const unsigned g = (unsigned)((a.T + 16 * AT_NW - 1) / (16 * AT_NW) * a.heads * B);
+            hipLaunchKernelGGL((psa_attention_lds<T>), dim3(g), dim3(64 * AT_NW), 0, s, a);
         }
         const long long n = (long long)B * a.T * (a.heads * DH / 8);
         hipLaunchKernelGGL((pe_add<T>), dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, a, B);
