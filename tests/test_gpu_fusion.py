@@ -101,15 +101,16 @@ def test_fused_stem_uint8_input(gpu, variant, dtype, batch, h, w):
 @pytest.mark.parametrize("variant,dtype,batch,h,w,nfused", [("n", torch.bfloat16, 2, 640, 640, 3),
                                                            ("n", torch.float16, 3, 96, 160, 3),
                                                            ("n", torch.bfloat16, 2, 608, 480, 3),
-                                                           ("n", torch.bfloat16, 1, 1280, 1280, 2),
-                                                           ("s", torch.float16, 2, 640, 640, 1),
+                                                           ("n", torch.bfloat16, 1, 1280, 1280, 0),
+                                                           ("s", torch.float16, 2, 640, 640, 0),
                                                            ("s", torch.bfloat16, 1, 1280, 1280, 0)])
 def test_c3k_block_equals_per_layer_launches(gpu, variant, dtype, batch, h, w, nfused):
     """c3k.hip: a CSPModule(c, c) block with c = 64 or 128 in one launch wherever bands of at
-    least 4 rows (+ the 4-row halo) fit a workgroup's LDS: v11_n's 40x40 (c = 64) net.p4.1 and
-    20x20 (c = 128) net.p5.1 / fpn.h6 at 640, only the 40x40 c = 128 ones at 1280 (80x80 bands
-    are too wide); v11_s's 40x40 c = 128 net.p4.1 at 640 (its 20x20 blocks have c = 256), none
-    at 1280. YH_C3K=0 keeps the seven per-layer launches everywhere. Bit-identical either way."""
+    least 4 rows (+ the 4-row halo) fit a workgroup's LDS, for c = 128 only where the bands allow
+    the SPLIT mode (phases within 8 pixel tiles): v11_n's 40x40 (c = 64) net.p4.1 and 20x20
+    (c = 128) net.p5.1 / fpn.h6 at 640 and 608x480 / 96x160, none at 1280 (80x80 c = 64 bands
+    are too wide, 40x40 c = 128 ones too tall for SPLIT); none for v11_s (40x40 c = 128, 20x20
+    c = 256). YH_C3K=0 keeps the seven per-layer launches everywhere. Bit-identical either way."""
     model = make_model(variant)
     x = synth.synth_scenes(batch, h, w, seed=37).to(gpu, dtype)
     fused = _engine(model, dtype, gpu, True)

@@ -554,8 +554,25 @@ void c3k_offsets(int hh, int (&off)[9]) {
     for (int i = 0; i < 9; ++i) off[i] = v[i];
 }
 
+// h = 64 runs fused only with bands that allow the SPLIT mode: its one-group form measured
+// slower than the seven launches at 40 x 40 (v11_s b64: 138 vs 129 us; bench on / off equal)
+static bool ck_split_fits(int H, int W, int r) {
+    return ck_live_px(H, W, r) <= 32 * 8 &&
+           ck_lds_px(64, ck_region_px(H, W, r), 4, (long long)((H + r - 1) / r) * W) <= 160 * 1024;
+}
+static int ck_split_bands(int H, int W, int r) {   // the first band count >= r that fits, else 0
+    for (r = std::max(1, r); r <= H; ++r)
+        if (ck_split_fits(H, W, r)) return r;
+    return 0;
+}
+
 int c3k_lds(int H, int W, int hh) {
     if (H < 1 || W < 1 || (hh != 32 && hh != 64)) return 0;
+    if (hh == 64) {
+        const int r = ck_split_bands(H, W, 1);
+        if (r == 0 || (r > 1 && (H + r - 1) / r < CK_MINRB)) return 0;
+        return (int)ck_lds_px(64, ck_region_px(H, W, r), 4, (long long)((H + r - 1) / r) * W);
+    }
     // the fewest bands that fit; bands of fewer than CK_MINRB rows recompute too much halo
     const int r = ck_fit_bands(hh, H, W, 1);
     const int rpx = ck_region_px(H, W, r);
@@ -571,6 +588,8 @@ int c3k_bands(int B, int H, int W, int hh) {
     // more as the regions need to fit; YH_C3K_BANDS overrides the first choice
     int r = std::max(1, std::min((128 + B - 1) / B, H / CK_MINRB));
     if (const char* e = getenv("YH_C3K_BANDS")) r = std::max(1, std::min(atoi(e), H));
+    if (hh == 64)
+        if (const int rs = ck_split_bands(H, W, r)) return rs;
     return ck_fit_bands(hh, H, W, r);
 }
 
