@@ -207,12 +207,36 @@ def cpu_baseline(args, runs=3):
                        f"{threads} threads, torch.inference_mode()")
 
 
+def visible_gpus_without_hip():
+    """GPUs this process could use, counted without initialising HIP (the self-launch parent must
+    not: the ranks it spawns then start from a clean driver state). KFD topology nodes with SIMDs
+    are the GPUs; HIP_VISIBLE_DEVICES / ROCR_VISIBLE_DEVICES / CUDA_VISIBLE_DEVICES narrow them.
+    None when the topology is not readable (each rank then checks its own ordinal)."""
+    import glob
+    n = 0
+    try:
+        for f in glob.glob("/sys/class/kfd/kfd/topology/nodes/*/properties"):
+            with open(f) as fh:
+                props = dict(line.split()[:2] for line in fh if len(line.split()) >= 2)
+            if int(props.get("simd_count", "0")) > 0:
+                n += 1
+    except (OSError, ValueError):
+        return None
+    if n == 0:
+        return None
+    for var in ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        v = os.environ.get(var)
+        if v is not None:
+            n = min(n, len([t for t in v.split(",") if t.strip()]))
+    return n
+
+
 def launch_ranks(n, argv):
     """`bench.py --gpus N` (N > 1) started without a launcher: run N ranks, one per GPU, under
     torch.distributed.run as child processes and return its exit code. The reference's own
     multi-process entry is env-driven under a launcher (main.py:338-344, main.sh:1-2); here the
-    bench provides the launcher itself. This parent makes no GPU call (it only imports torch and
-    counts devices, which does not initialise HIP), so the ranks start from a clean process."""
+    bench provides the launcher itself. This parent makes no GPU call (it counts the GPUs from the
+    KFD topology, visible_gpus_without_hip), so the ranks start from a clean process."""
     import socket
     import subprocess
     with socket.socket() as s:
@@ -252,8 +276,9 @@ def main():
     args = ap.parse_args()
 
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
-        if not args.dry_run and torch.cuda.device_count() < args.gpus:
-            raise SystemExit(f"bench.py --gpus {args.gpus}: only {torch.cuda.device_count()} GPU(s) visible")
+        ngpu = None if args.dry_run else visible_gpus_without_hip()
+        if ngpu is not None and ngpu < args.gpus:
+            raise SystemExit(f"bench.py --gpus {args.gpus}: only {ngpu} GPU(s) visible")
         sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -266,6 +291,8 @@ def main():
         log(f"bench: --gpus {args.gpus} but the launcher started {world} rank(s); n_gpus = {world}")
     if args.dry_run:
         return dry_run(args, rank, world, dist)
+    if local >= torch.cuda.device_count():
+        raise SystemExit(f"bench.py rank {rank}: LOCAL_RANK {local} but only {torch.cuda.device_count()} GPU(s) visible")
     if dist:
         torch.cuda.set_device(local)
         torch.distributed.init_process_group("nccl", device_id=torch.device("cuda", local))

@@ -44,7 +44,7 @@
 extern "C" {
 #endif
 
-#define YH_ABI_VERSION 3
+#define YH_ABI_VERSION 4
 
 /* status codes */
 #define YH_OK 0
@@ -222,6 +222,29 @@ int yh_force_conv_kernel(yh_handle* h, int kernel);
 int yh_unit_count(const yh_handle* h, int batch, int height, int width);
 int yh_unit_info(const yh_handle* h, int index, int batch, int height, int width, int* first_op,
                  int* num_ops, int* is_level, double* ms_total, int* calls);
+
+/* Parity taps (tests/test_gpu_op_parity.py; no reference counterpart: they expose the
+ * per-module intermediates nets/nn.py:28-270 computes, so each fused / 16-bit kernel can be
+ * checked against the fp64 oracle on its own device-produced inputs).
+ *
+ * yh_debug_op_desc writes a JSON description of op `index` at (batch, height, width) into buf
+ * (NUL-terminated; returns its length, or a negative status): kind, label, "active" (1 if the
+ * op launches at this shape, 0 if a fused alternative replaces it, -1 before the first
+ * yh_forward there), the convs it computes ({name, k, s, g, act, cin, cout, bias}, in the
+ * op's order, null for an absent one) and its workspace operands ({role, H, W, C, logical,
+ * up}: inputs "in0"/"in1"/"res"/"x<l>"/"L<l>", outputs "out"/"y<l>"; an op whose output
+ * is the caller's y, or whose input is the caller's x, lists no operand for it).
+ *
+ * yh_debug_run_ops launches the active ops in [first, last) eagerly on `stream`, after a
+ * yh_forward at the same shape (x_u8: x is the uint8 image tensor). Running 0..n in steps
+ * reproduces yh_forward's workspace and y exactly.
+ *
+ * yh_debug_operand copies operand `slot` (the desc's order) of op `index` out of the
+ * workspace into dst as a dense (batch, H, W, C) array of the handle dtype, async on stream. */
+int yh_debug_op_desc(const yh_handle* h, int index, int batch, int height, int width, char* buf, size_t size);
+int yh_debug_run_ops(yh_handle* h, const void* x, int x_u8, int batch, int height, int width, void* y, int first,
+                     int last, void* stream);
+int yh_debug_operand(const yh_handle* h, int index, int slot, void* dst, void* stream);
 
 #ifdef __cplusplus
 }

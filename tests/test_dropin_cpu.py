@@ -55,6 +55,21 @@ def test_module_forward_matches_golden_fp32():
     np.testing.assert_allclose(y, g["y"], rtol=1e-5, atol=2e-3)
 
 
+def test_module_forward_matches_golden_fp32_c1():
+    """C1's own shape (BASELINE.json configs[0]: v11_n, 1 x 3 x 640 x 640, PyTorch CPU forward)
+    through the drop-in module on the CPU, against the reference's float64 golden, within
+    2x the reference's own fp32 noise (8 vs 1 thread) in pixels and scores."""
+    g = load_golden(golden_name("n", 640, 1))
+    m = make_model("n")
+    x = synth.synth_scenes(1, 640, 640, seed=GOLDEN_INPUT_SEED)
+    with torch.no_grad():
+        y = m(x).double().numpy()
+    d = np.abs(y - g["y"])
+    noise = [float(v) for v in g["dev_fp32_8thr"]]
+    assert d[:, :4].max() <= max(1e-3, 2 * noise[0]), (d[:, :4].max(), noise[0])
+    assert d[:, 4:].max() <= max(1e-5, 2 * noise[2]), (d[:, 4:].max(), noise[2])
+
+
 def test_fuse_matches_reference_fold_formula():
     from nets import nn
     conv = torch.nn.Conv2d(8, 16, 3, padding=1, bias=False)

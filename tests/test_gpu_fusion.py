@@ -211,13 +211,14 @@ def test_attention_full_kernel_equals_chunked_kernel_and_pe_add(gpu, variant, dt
 @pytest.mark.parametrize("variant,dtype,batch,size", [("n", torch.bfloat16, 4, 640), ("s", torch.float16, 2, 320),
                                                       ("x", torch.bfloat16, 1, 1280), ("n", torch.float16, 2, 224)])
 def test_sppf_kernel_equals_three_maxpools(gpu, variant, dtype, batch, size):
-    """misc.hip sppf_fused (CPW 8-channel chunks of one image per workgroup, chosen by the LDS:
-    8 at 20x20, 2 at 40x40) and with one chunk per workgroup (YH_SPPF_CPW=1) are bit-identical
-    to three maxpool5 launches (YH_SPPF_FUSED=0). Both switches are read at launch."""
+    """misc.hip sppf_fused (CPW 8-channel chunks of one image per workgroup: 2 by default, halved
+    until the planes fit the LDS) with 1, 2 (default), 4 and 8 chunks (YH_SPPF_CPW; 8 fits at
+    20x20, 40x40 falls back to 2) is bit-identical to three maxpool5 launches (YH_SPPF_FUSED=0).
+    Both switches are read at launch."""
     model = make_model(variant)
     x = synth.synth_scenes(batch, size, size, seed=35).to(gpu, dtype)
     ys = []
-    for env in ({"YH_SPPF_FUSED": "0"}, {"YH_SPPF_CPW": "1"}, {}):
+    for env in ({"YH_SPPF_FUSED": "0"}, {"YH_SPPF_CPW": "1"}, {}, {"YH_SPPF_CPW": "4"}, {"YH_SPPF_CPW": "8"}):
         old = {k: os.environ.get(k) for k in ("YH_SPPF_FUSED", "YH_SPPF_CPW")}
         os.environ.update(env)
         try:
@@ -231,16 +232,18 @@ def test_sppf_kernel_equals_three_maxpools(gpu, variant, dtype, batch, size):
                 else:
                     os.environ[k] = v
     assert torch.isfinite(ys[0].float()).all()
-    assert torch.equal(ys[0], ys[1]) and torch.equal(ys[0], ys[2])
+    for yv in ys[1:]:
+        assert torch.equal(ys[0], yv)
 
 
 @pytest.mark.parametrize("bands", ["1", "2", "3", "5", "7", "20"])
 def test_c3k_row_bands_equal_per_layer_launches(gpu, bands):
     """c3k.hip row bands: each image's block is split over `bands` workgroups that recompute the
-    4-row halo of the chain of four 3x3 convs; every split (1 = one workgroup per image, 20 =
-    one row each at 20x20, uneven splits, a last band with no rows; the 40x40 block takes at
-    least the 10 bands its regions need) is bit-identical to the seven per-layer launches.
-    YH_C3K_BANDS is read at launch."""
+    4-row halo of the chain of four 3x3 convs; every split (1 = one workgroup per image where the
+    region fits, 20 = one row each at 20x20, uneven splits, a last band with no rows; the 40x40
+    h = 32 block takes at least the 10 bands its regions need and the 20x20 h = 64 blocks at least
+    the 4 bands of their SPLIT mode, the only mode h = 64 runs in) is bit-identical to the seven
+    per-layer launches. YH_C3K_BANDS is read at launch."""
     model = make_model("n")
     x = synth.synth_scenes(2, 640, 640, seed=38).to(gpu, torch.bfloat16)
     plain = _engine(model, torch.bfloat16, gpu, True, YH_C3K="0")

@@ -519,11 +519,11 @@ int launch_c3k_t(const C3kArgs& a0, hipStream_t s) {
     C3kArgs a = a0;
     a.bands = c3k_bands(a.B, a.H, a.W, HH);
     const int rpx = ck_region_px(a.H, a.W, a.bands), bpx = (a.H + a.bands - 1) / a.bands * a.W;
-    // SPLIT where phases B..F fit 8 tiles and the ring keeps >= 4 buffers beside conv2's
-    // band (YH_C3K_SPLIT=0: never); as many ring buffers as the LDS holds (YH_C3K_NB: fewer)
-    static const bool split_ok = [] { const char* e = getenv("YH_C3K_SPLIT"); return !e || atoi(e) != 0; }();
-    const bool split = HH == 64 && split_ok && ck_live_px(a.H, a.W, a.bands) <= 32 * 8 &&
-                       ck_lds_px(HH, rpx, 4, bpx) <= 160 * 1024;
+    // h = 64 runs only in SPLIT mode (phases B..F within 8 tiles, the ring keeping >= 4 buffers
+    // beside conv2's band: c3k_lds / c3k_bands admit no other h = 64 shape); as many ring buffers
+    // as the LDS holds (YH_C3K_NB: fewer)
+    const bool split = HH == 64 && ck_live_px(a.H, a.W, a.bands) <= 32 * 8 && ck_lds_px(HH, rpx, 4, bpx) <= 160 * 1024;
+    if (HH == 64 && !split) return (int)hipErrorInvalidValue;
     const long long bp = split ? bpx : 0;
     a.nbuf = 2;
     while (a.nbuf < CK_MAXNB && ck_lds_px(HH, rpx, a.nbuf + 1, bp) <= 160 * 1024) ++a.nbuf;
@@ -532,11 +532,11 @@ int launch_c3k_t(const C3kArgs& a0, hipStream_t s) {
     if (c3k_lds(a.H, a.W, HH) == 0 || ck_live_px(a.H, a.W, a.bands) > 32 * CK_NW || rpx > 2 * 32 * CK_NW ||
         lds > 160 * 1024 || a.B < 1 || a.ldx % 8 || a.ldy % 8)
         return (int)hipErrorInvalidValue;
-    auto k = split ? &c3k_fused<T, HH, HH == 64> : &c3k_fused<T, HH, false>;
-    static bool attr[2] = {false, false};
-    if (!attr[split]) {
+    auto k = &c3k_fused<T, HH, HH == 64>;
+    static bool attr = false;
+    if (!attr) {
         (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-        attr[split] = true;
+        attr = true;
     }
     hipLaunchKernelGGL(k, dim3((unsigned)(a.B * a.bands)), dim3(CK_THREADS), (int)lds, s, a);
     return (int)hipGetLastError();

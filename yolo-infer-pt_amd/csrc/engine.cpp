@@ -1648,6 +1648,130 @@ struct Net {
         }
     }
 
+    // ---------------------------------------------------------- parity taps (tests only)
+    // The workspace operands of an op, in a fixed order (yh_debug_op_desc lists them):
+    // inputs first, then outputs. `logical` = channels the op reads / writes of the view.
+    struct Operand { std::string role; View v; int up = 0; int logical = 0; };
+    std::vector<Operand> operands(const Op& op) const {
+        std::vector<Operand> r;
+        auto add = [&](const std::string& role, const View& v, int up, int logical) {
+            Operand o;
+            o.role = role; o.v = v; o.up = up; o.logical = logical;
+            r.push_back(o);
+        };
+        switch (op.kind) {
+            case OP_CONV: {
+                const ConvDesc& d = convs[op.conv];
+                for (size_t si = 0; si < op.in.size(); ++si)
+                    add("in" + std::to_string(si), op.in[si].v, op.in[si].up, d.segs[si].first);
+                if (op.has_res) add("res", op.res, 0, d.cout);
+                add("out", op.out, 0, d.cout);
+                break;
+            }
+            case OP_FIRST: case OP_STEM2: add("out", op.out, 0, op.out.C); break;
+            case OP_DW: case OP_ATTN: case OP_CSP: case OP_C3K:
+                add("in0", op.in[0].v, op.in[0].up, op.in[0].v.C);
+                add("out", op.out, 0, op.out.C);
+                break;
+            case OP_SPPF: {
+                View o = op.out;
+                o.coff += op.out.C;
+                o.C = 3 * op.out.C;
+                add("in0", op.out, 0, op.out.C);
+                add("out", o, 0, o.C);
+                break;
+            }
+            case OP_HEADCLS:
+                for (int l = 0; l < 3; ++l)
+                    if (op.hlv[l]) add("x" + std::to_string(l), op.hx[l], 0, op.hx[l].C);
+                if (!op.direct)
+                    for (int l = 0; l < 3; ++l)
+                        if (op.hlv[l]) add("y" + std::to_string(l), op.hy[l], 0, var.num_classes);
+                break;
+            case OP_BOXDFL:
+                for (int l = 0; l < 3; ++l) add("x" + std::to_string(l), op.bx[l], 0, op.bx[l].C);
+                break;
+            case OP_DECODE:
+                for (int l = 0; l < 3; ++l) add("L" + std::to_string(l), op.lvl[l], 0, 64 + var.num_classes);
+                break;
+        }
+        return r;
+    }
+    // the convs an op computes, in the op's order (-1: none in that place, e.g. tail-mode conv1)
+    std::vector<int> op_convs(const Op& op) const {
+        switch (op.kind) {
+            case OP_CONV: case OP_FIRST: case OP_DW: case OP_ATTN: return {op.conv};
+            case OP_STEM2: return {op.conv, op.cs[0]};
+            case OP_CSP: return {op.cs[0], op.cs[1], op.cs[2], op.cs[3]};
+            case OP_C3K: return std::vector<int>(op.ck, op.ck + 7);
+            case OP_HEADCLS: {
+                std::vector<int> r;
+                for (int l = 0; l < 3; ++l)
+                    for (int k = 0; k < 5; ++k) r.push_back(op.hlv[l] ? op.hc[l][k] : -1);
+                return r;
+            }
+            case OP_BOXDFL: return {op.bc[0], op.bc[1], op.bc[2]};
+            case OP_SPPF: case OP_DECODE: return {};
+        }
+        return {};
+    }
+    std::string op_desc(int oi, int B, int H, int W) const {
+        const Op& op = ops[oi];
+        auto it = plans.find(GraphKey{B, H, W});
+        const int active = it == plans.end() ? -1 : it->second.active[oi];
+        std::string s = "{\"index\": " + std::to_string(oi) + ", \"kind\": \"" + op_kind_name(op.kind) +
+                        "\", \"label\": \"" + op.label + "\", \"active\": " + std::to_string(active) +
+                        ", \"heads\": " + std::to_string(op.heads) + ", \"direct\": " + std::to_string(op.direct ? 1 : 0) +
+                        ", \"dlo\": " + std::to_string(op.dlo) + ", \"dbox\": " + std::to_string(op.dbox ? 1 : 0) +
+                        ", \"convs\": [";
+        const std::vector<int> cv = op_convs(op);
+        for (size_t i = 0; i < cv.size(); ++i) {
+            if (i) s += ", ";
+            if (cv[i] < 0) { s += "null"; continue; }
+            const ConvDesc& d = convs[cv[i]];
+            s += "{\"name\": \"" + d.name + "\", \"k\": " + std::to_string(d.k) + ", \"s\": " + std::to_string(d.stride) +
+                 ", \"g\": " + std::to_string(d.groups) + ", \"act\": " + std::to_string(d.act) + ", \"cin\": " +
+                 std::to_string(d.cin) + ", \"cout\": " + std::to_string(d.cout) + ", \"bias\": " +
+                 std::to_string(d.has_bias) + "}";
+        }
+        s += "], \"operands\": [";
+        const std::vector<Operand> od = operands(op);
+        for (size_t i = 0; i < od.size(); ++i) {
+            const int lv = tensors[od[i].v.t].level;
+            s += std::string(i ? ", " : "") + "{\"role\": \"" + od[i].role + "\", \"H\": " + std::to_string(H >> lv) +
+                 ", \"W\": " + std::to_string(W >> lv) + ", \"C\": " + std::to_string(od[i].v.C) + ", \"logical\": " +
+                 std::to_string(od[i].logical) + ", \"up\": " + std::to_string(od[i].up) + "}";
+        }
+        s += "]}";
+        return s;
+    }
+    // the active ops in [first, last) of the forward at (B, H, W), launched eagerly on s
+    void debug_run(const void* x, int x_u8, int B, int H, int W, void* y, int first, int last, hipStream_t s) {
+        in_u8 = x_u8;
+        for (auto& d : convs) require(d.loaded, "weights of " + d.name + " not loaded", YH_ESTATE);
+        require(ws.base && ws.B == B && ws.H == H && ws.W == W, "yh_debug_run_ops: run yh_forward at this shape first",
+                YH_ESTATE);
+        require(first >= 0 && first <= last && last <= (int)ops.size(), "op range out of bounds");
+        HIPCHECK(hipSetDevice(device));
+        require(launch_set_io(io_dev, x, y, s) == 0, "set_io launch failed", YH_EHIP);
+        ensure_plan(B, H, W);
+        ensure_tuned(B, H, W, s);
+        for (int i = first; i < last; ++i)
+            if (cur_plan->active[i]) launch_op((size_t)i, B, H, W, s);
+    }
+    // operand `slot` of op `oi` copied out of the workspace as a dense (B, h, w, C) array
+    void debug_operand(int oi, int slot, void* dst, hipStream_t s) const {
+        require(oi >= 0 && oi < (int)ops.size(), "op index out of range");
+        const std::vector<Operand> od = operands(ops[oi]);
+        require(slot >= 0 && slot < (int)od.size(), "operand slot out of range");
+        require(ws.base != nullptr, "no workspace yet", YH_ESTATE);
+        const View& v = od[slot].v;
+        const int lv = tensors[v.t].level;
+        const size_t rows = (size_t)ws.B * (ws.H >> lv) * (ws.W >> lv);
+        HIPCHECK(hipMemcpy2DAsync(dst, (size_t)v.C * es, ptr(v), (size_t)ldc(v) * es, (size_t)v.C * es, rows,
+                                  hipMemcpyDeviceToDevice, s));
+    }
+
     ~Net() {
         drop_graphs();
         free_plans();
@@ -1940,6 +2064,34 @@ int yh_force_conv_kernel(yh_handle* h, int kernel) {
         h->net.conv_kern.clear();
         h->net.cur_kern = nullptr;
         h->net.drop_graphs();
+    });
+}
+
+int yh_debug_op_desc(const yh_handle* h, int index, int batch, int height, int width, char* buf, size_t size) {
+    int len = 0;
+    const int rc = guarded([&] {
+        yh::require(h && index >= 0 && index < (int)h->net.ops.size(), "op index out of range");
+        const std::string s = h->net.op_desc(index, batch, height, width);
+        yh::require(buf && size > s.size(), "buffer too small");
+        std::memcpy(buf, s.c_str(), s.size() + 1);
+        len = (int)s.size();
+    });
+    return rc == YH_OK ? len : rc;
+}
+
+int yh_debug_run_ops(yh_handle* h, const void* x, int x_u8, int batch, int height, int width, void* y, int first,
+                     int last, void* stream) {
+    return guarded([&] {
+        yh::require(h && x && y, "null argument");
+        h->net.debug_run(x, x_u8, batch, height, width, y, first, last, (hipStream_t)stream);
+    });
+}
+
+int yh_debug_operand(const yh_handle* h, int index, int slot, void* dst, void* stream) {
+    return guarded([&] {
+        yh::require(h && dst, "null argument");
+        HIPCHECK(hipSetDevice(h->net.device));
+        h->net.debug_operand(index, slot, dst, (hipStream_t)stream);
     });
 }
 

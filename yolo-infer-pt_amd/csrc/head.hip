@@ -570,8 +570,25 @@ int launch_box_dfl(int dtype, const BoxDflArgs& a, hipStream_t s) {
     return (int)hipErrorInvalidValue;
 }
 
+// every hc_div / hc_q quotient of a TH x TW tile is exact (n < 2^s / d for each divisor d and
+// numerator range n the kernel uses), so a larger tile added to head_cls_tile cannot silently
+// index the wrong rows
+static bool hc_div_exact(int TH, int TW, int C0, int c3, int nc) {
+    const long long XH = TH + 4, XW = TW + 4, MH = TH + 2, MW = TW + 2;
+    if (XH * XW * XW >= (1 << 16) || MH * MW * MW >= (1 << 16) || (long long)TH * TW * TW >= (1 << 16)) return false;
+    const int ng1 = (C0 < HC_CK ? C0 : HC_CK) / 4, ng2 = c3 / 4;
+    for (int k = 0; k < 2; ++k) {   // the two depthwise phases: MH x MW (dw1) and TH x TW (dw2)
+        const long long DH = k ? TH : MH, DW = k ? TW : MW, ng = k ? ng2 : ng1;
+        const long long per_g = DW * ((DH + HC_RB - 1) / HC_RB);
+        if (DW * per_g >= (1 << 16) || ng * per_g * per_g >= (1 << 24)) return false;
+    }
+    const long long na = (std::max(c3, nc) + 31) / 32, nb = (MH * MW + 31) / 32;
+    return na * nb * na < (1 << 16);
+}
+
 int head_cls_lds(int TH, int TW, int C0, int c3, int nc) {
     if (C0 % 64 && C0 > 64) return 0;            // whole 64-channel chunks
+    if (!hc_div_exact(TH, TW, C0, c3, nc)) return 0;
     // instantiated: C0 64 / 128 / 256, c3 64 / 80, at most three 32-cout tiles per pointwise conv
     if (!(C0 == 64 || C0 == 128 || C0 == 256) || !(c3 == 64 || c3 == 80) || nc > 32 * HC_NA) return 0;
     // parameter chunks: 10 (C0 + c3) / 4 + 72 <= 4 per thread

@@ -126,8 +126,9 @@ int launch_sppf_t(const PoolArgs& a, hipStream_t s) {
                                           hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
                 attr_set = true;
             }
-            // chunks per workgroup: the most of 8 / 4 / 2 / 1 that divides the channels and whose
-            // two planes fit the LDS (YH_SPPF_CPW: at most that many)
+            // chunks per workgroup: 2 (YH_SPPF_CPW: another count; 4 / 8 ran 47 / 86 us against
+            // 29 us for one chunk), halved until it divides the channels and
+            // the three planes fit the LDS
             const char* e = getenv("YH_SPPF_CPW");
             int cpw = e ? std::max(1, atoi(e)) : 2;
             while (cpw > 1 && ((a.C / 8) % cpw || 3 * a.H * a.W * cpw * 16 > 160 * 1024))

@@ -195,6 +195,32 @@ class Engine:
         return out
 
 
+    # ------------------------------------------------------------------ parity taps (tests)
+    def debug_op_desc(self, index, batch, height, width):
+        """JSON description of op `index` at this shape (kind, convs, workspace operands)."""
+        import json
+        buf = ctypes.create_string_buffer(1 << 16)
+        rc = lib().yh_debug_op_desc(self._h, int(index), int(batch), int(height), int(width), buf, len(buf))
+        if rc < 0:
+            check(rc, "debug_op_desc")
+        return json.loads(buf.value.decode())
+
+    def debug_run(self, x, y, first, last):
+        """Launch the active ops in [first, last) eagerly (after a forward at x's shape)."""
+        B, _, H, W = x.shape
+        check(lib().yh_debug_run_ops(self._h, c_void_p(x.data_ptr()), int(x.dtype == torch.uint8), B, H, W,
+                                     c_void_p(y.data_ptr()), int(first), int(last), _stream_ptr(x.device)),
+              "debug_run")
+
+    def debug_operand(self, index, slot, batch, desc):
+        """Operand `slot` of op `index` as a dense (batch, H, W, C) tensor of the engine dtype."""
+        o = desc["operands"][slot]
+        out = torch.empty((batch, o["H"], o["W"], o["C"]), dtype=self.dtype, device=self.device)
+        check(lib().yh_debug_operand(self._h, int(index), int(slot), c_void_p(out.data_ptr()),
+                                     _stream_ptr(self.device)), "debug_operand")
+        return out
+
+
 class _BN:
     def __init__(self, weight, bias, mean, var, eps):
         self.weight, self.bias, self.running_mean, self.running_var, self.eps = weight, bias, mean, var, eps
