@@ -191,7 +191,8 @@ int yh_op_count(const yh_handle* h);
 /* Describe op `index` for an input of (batch, height, width): label (module
  * path), class (0 dense 3x3 conv, 1 dense 1x1 conv, 2 stem conv, 3 depthwise,
  * 4 SPPF pools, 5 PSA attention, 6 head decode, 7 fused head cls branch,
- * 8 fused box tail with DFL, 9 fused C3k2 block, 10 fused C3k block), algorithmic bytes (each
+ * 8 fused box tail with DFL, 9 fused C3k2 block, 10 fused C3k block, 11 fused box branch of all
+ * levels), algorithmic bytes (each
  * operand read once, each output written once, handle dtype) and FLOPs per
  * call, accumulated profiled milliseconds and call count. */
 int yh_op_info(const yh_handle* h, int index, int batch, int height, int width,

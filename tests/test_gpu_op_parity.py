@@ -19,7 +19,7 @@ Covered kernels (by configuration):
   * C2 v11_n bf16 640 b32 (images 0, 17, 31): the tuned conv_mx / conv_mxr / conv_rw plans incl.
     the K-split ones (20x20 / 40x40 layers), stem_fused, csp_fused (whole-block and tail mode),
     c3k_fused in row bands and in SPLIT mode, sppf_fused, psa_attention_full, head_cls (all three
-    levels, scores written straight into y), box_dfl;
+    levels, scores written straight into y), box_chain (the whole box branch of the three levels);
   * v11_n fp16 640 b2: the same kernels in fp16;
   * C3 v11_s fp16 640 b64 (images 0, 63): wider conv plans, seven-launch C3k, per-layer cls
     branches (dwconv3x3_c4) and the class-rows decode (head_decode_lds);
@@ -114,6 +114,17 @@ def _check_op(d, ins, outs, x, y, H, W, nc, params, dtype):
             fn = lambda l=l: oc.dfl_box(*oc.layer(ins[f"x{l}"], ins[f"x{l}"], d["convs"][l], params, dtype), 8 << l,
                                         dtype)
             cases.append((f"level {l} boxes", y[:, 0:4, a0:a0 + h * w], fn))
+    elif kind == "box_chain":
+        for l in range(3):
+            h, w = H >> (3 + l), W >> (3 + l)
+            a0 = _anchor_off(l, H, W)
+            c0, c1, c2 = d["convs"][3 * l:3 * l + 3]
+
+            def fn(l=l, c0=c0, c1=c1, c2=c2):
+                lo, hi = oc.layer(ins[f"x{l}"], ins[f"x{l}"], c0, params, dtype)
+                lo, hi = oc.layer(lo, hi, c1, params, dtype)
+                return oc.dfl_box(*oc.layer(lo, hi, c2, params, dtype), 8 << l, dtype)
+            cases.append((f"level {l} boxes", y[:, 0:4, a0:a0 + h * w], fn))
     elif kind == "decode":
         for l in range(3):
             L = ins[f"L{l}"]
@@ -181,7 +192,7 @@ def run_op_parity(gpu, variant, dtype, batch, size, images, seed):
             # chains, where a layer's undecided roundings (1 ulp either way, both legitimate) feed
             # the next layer's K-sum, nor for attention, whose softmax weights are rounded to the
             # dtype for the P.V MFMA (r05: 2-6 % of its outputs; the interval accounts for both)
-            multi = d["kind"] in ("stem_fused", "c3k2", "c3k", "head_cls", "attention")
+            multi = d["kind"] in ("stem_fused", "c3k2", "c3k", "head_cls", "box_chain", "attention")
             if s["bad"] or (not multi and s["over1"] > 1e-3):
                 failures.append((d["label"], kernels[i], s))
     assert not failures, failures[:4]
@@ -192,19 +203,20 @@ def run_op_parity(gpu, variant, dtype, batch, size, images, seed):
 
 def test_op_parity_c2_n_bf16_b32(gpu):
     kinds, n = run_op_parity(gpu, "n", torch.bfloat16, 32, 640, (0, 17, 31), seed=21)
-    assert {"stem_fused", "conv", "c3k2", "c3k", "sppf", "attention", "head_cls", "box_dfl"} <= kinds, kinds
+    assert {"stem_fused", "conv", "c3k2", "c3k", "sppf", "attention", "head_cls", "box_chain"} <= kinds, kinds
 
 
 def test_op_parity_n_fp16(gpu):
     kinds, n = run_op_parity(gpu, "n", torch.float16, 2, 640, (0, 1), seed=22)
-    assert {"stem_fused", "conv", "c3k2", "c3k", "sppf", "attention", "head_cls", "box_dfl"} <= kinds, kinds
+    assert {"stem_fused", "conv", "c3k2", "c3k", "sppf", "attention", "head_cls", "box_chain"} <= kinds, kinds
 
 
 def test_op_parity_c3_s_fp16_b64(gpu):
     kinds, n = run_op_parity(gpu, "s", torch.float16, 64, 640, (0, 63), seed=23)
-    assert {"stem_fused", "conv", "c3k2", "dwconv", "decode", "box_dfl", "attention", "sppf"} <= kinds, kinds
+    assert {"stem_fused", "conv", "c3k2", "dwconv", "decode", "box_chain", "attention", "sppf"} <= kinds, kinds
 
 
 def test_op_parity_c5_x_bf16_1280(gpu):
     kinds, n = run_op_parity(gpu, "x", torch.bfloat16, 1, 1280, (0,), seed=24)
     assert {"stem", "conv", "dwconv", "decode", "box_dfl", "attention", "sppf"} <= kinds, kinds
+    # (x: 96 box channels, the per-layer box convs + box_dfl)

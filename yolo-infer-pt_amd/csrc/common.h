@@ -236,6 +236,30 @@ int launch_csp(int dtype, const CspArgs& a, int grid, hipStream_t s);
 constexpr int BOX_DFL_TPW = 4;       // 32-pixel tiles per wave (4 waves per workgroup)
 int launch_box_dfl(int dtype, const BoxDflArgs& a, hipStream_t s);
 
+// The whole box branch of the detect head (boxc.hip), one launch for all levels: box.l.0 (3x3
+// C0 -> 64) -> box.l.1 (3x3 64 -> 64) -> box.l.2 (1x1 64 -> 64 + bias) -> DFL + anchors +
+// dist2bbox into rows 0..3 of y = io[1] (nets/nn.py:240-247, 222-225, 255-270), the two 64-channel
+// intermediates only in LDS. Bit-identical to the per-layer launches + box_dfl.
+struct BoxChainLevel {
+    const void* x; int ldx, C0;      // box.l.0 input (NHWC view), its channels (64 / 128 / 256 / 512)
+    int H, W;
+    int TH, TW, ntw, tiles;          // output tile, tiles per row / per image (bx_tile)
+    int nkc;                         // box.l.0's K chunks (mx_kchunks of its shape: 1 or C0 / 64)
+    float stride; int aoff;          // the level's stride and first anchor
+    const void* prm;                 // packed parameters (bx_prm_bytes(C0))
+    int wg0;                         // first workgroup of the level (one per tile)
+};
+struct BoxChainArgs {
+    BoxChainLevel lv[3];
+    int nlv, B, nc, A;
+    const void* const* io;
+    const void* zero;                // >= 256 zero bytes
+};
+int bx_prm_bytes(int C0);
+bool bx_ok(int C0);
+bool bx_tile(int H, int W, int& TH, int& TW);
+int launch_box_chain(int dtype, const BoxChainArgs& a, hipStream_t s);
+
 // launchers (return hipError_t as int)
 bool conv_kernel_ok(int dtype, int kern, const ConvArgs& a);
 int launch_conv(int dtype, int kern, int BM, int BN, const ConvArgs& a, hipStream_t s);

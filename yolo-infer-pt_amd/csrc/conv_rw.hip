@@ -134,7 +134,8 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t rw_rsrc(const void* base) {
 }  // namespace
 
 template <typename T, int S, int CIN, int NCG, int NPG, int MB, int TW, int NS, bool RES, int NKC>
-__global__ __launch_bounds__(64 * NCG * NKC * NPG, NCG * NKC * NPG >= 8 ? 2 : 1) void conv_rw(const MxArgs p) {
+__global__ __launch_bounds__(64 * NCG * NKC * NPG, (NCG * NKC * NPG >= 8 || NCG > 1 || CIN <= 32) ? 2 : 1) void conv_rw(
+    const MxArgs p) {
     constexpr int NW = NCG * NKC * NPG;
     constexpr int CPP = CIN / 8;                 // 16-B chunks per input pixel
     constexpr int NKT = CIN / 16 * 9;            // k-steps of the whole walk (canonical: cb, then tap)
@@ -523,9 +524,11 @@ MxPlan mx_plan_w(const MxShape& sh, const MxConfig& c, int num_cus) {
             if (cf < best) { best = cf; bsh = s2; bmr = mr; }
         }
     pl.sw_sh = bsh; pl.sw_mr = bmr; pl.conflicts = best;
-    // Cin = 64: the weights take ~150 of a lane's VGPRs, one workgroup per CU; Cin <= 32
-    // 4-wave workgroups fit two per CU
-    const int per_cu = std::max(1, std::min((160 * 1024) / pl.lds, sh.cin <= 32 && g.nw == 4 ? 2 : 1));
+    // every kernel keeps <= 256 VGPRs (2 waves per SIMD): 4-wave workgroups run two per CU where
+    // the LDS allows, so each SIMD's two waves come from different workgroups and drift apart
+    // (one's epilogue / barrier wait beside the other's MFMAs); 8-wave ones run one per CU
+    const bool two = g.nw == 4 && (ncg > 1 || sh.cin <= 32);   // (the 1-cout-group Cin 64 kernel needs > 256)
+    const int per_cu = std::max(1, std::min((160 * 1024) / pl.lds, two ? 2 : 1));
     // every wave loads its cout group's whole weight image: fewer, longer-lived workgroups
     // (gdiv) trade parallelism for weight traffic on small layers
     const int wps = std::max(1, std::min(pl.ntasks, per_cu * num_cus / pl.nslices) / std::max(1, c.gdiv));
@@ -564,7 +567,7 @@ void mx_candidates_w(const MxShape& sh, std::vector<MxConfig>& out) {
         }
     } else if (sh.s == 1) {
         if (sh.cin == 64 && ncg == 2) {
-            add(2, 4, 1, 16, 4); add(2, 4, 1, 8, 4); add(2, 2, 1, 8, 4); add(2, 2, 1, 4, 4);
+            add(2, 4, 1, 16, 4); add(2, 4, 1, 8, 4); add(2, 2, 1, 8, 4); add(2, 2, 1, 4, 4); add(2, 2, 1, 8, 3);
         } else if (sh.cin == 64 && ncg == 1) {
             add(1, 8, 1, 16, 3); add(1, 4, 1, 8, 4);
         } else if (sh.cin == 32 && ncg == 1) {
@@ -643,6 +646,7 @@ int launch_rw_cfg(const MxPlan& pl, const MxArgs& a, hipStream_t s) {
     YH_RW(1, 64, 2, 4, 1, 8, 4, 1)
     YH_RW(1, 64, 2, 2, 1, 8, 4, 1)
     YH_RW(1, 64, 2, 2, 1, 4, 4, 1)
+    YH_RW(1, 64, 2, 2, 1, 8, 3, 1)
     YH_RW(1, 64, 1, 8, 1, 16, 3, 1)
     YH_RW(1, 64, 1, 4, 1, 8, 4, 1)
     YH_RW(1, 32, 1, 4, 1, 8, 4, 1)

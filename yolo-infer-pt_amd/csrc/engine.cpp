@@ -75,7 +75,8 @@ static uint16_t f2h(float f) {
 
 // ---------------------------------------------------------------- graph model
 enum ConvKind { CK_DENSE = 0, CK_FIRST = 1, CK_DW = 2, CK_PE = 3 };
-enum OpKind { OP_FIRST, OP_CONV, OP_DW, OP_SPPF, OP_ATTN, OP_DECODE, OP_HEADCLS, OP_BOXDFL, OP_CSP, OP_STEM2, OP_C3K };
+enum OpKind { OP_FIRST, OP_CONV, OP_DW, OP_SPPF, OP_ATTN, OP_DECODE, OP_HEADCLS, OP_BOXDFL, OP_CSP, OP_STEM2, OP_C3K,
+              OP_BOXCHAIN };
 static const char* op_kind_name(OpKind k) {
     switch (k) {
         case OP_FIRST: return "stem";
@@ -89,11 +90,12 @@ static const char* op_kind_name(OpKind k) {
         case OP_CSP: return "c3k2";
         case OP_C3K: return "c3k";
         case OP_STEM2: return "stem_fused";
+        case OP_BOXCHAIN: return "box_chain";
     }
     return "unknown";
 }
 enum OpClass { CL_CONV3 = 0, CL_CONV1 = 1, CL_FIRST = 2, CL_DW = 3, CL_SPPF = 4, CL_ATTN = 5, CL_DECODE = 6,
-               CL_HEADCLS = 7, CL_BOXDFL = 8, CL_CSP = 9, CL_C3K = 10, CL_N = 11 };
+               CL_HEADCLS = 7, CL_BOXDFL = 8, CL_CSP = 9, CL_C3K = 10, CL_BOXCHAIN = 11, CL_N = 12 };
 
 struct Tensor { int level; int C; };        // physical channels = pixel stride
 struct View { int t = -1; int coff = 0; int C = 0; };
@@ -142,6 +144,10 @@ struct Op {
     // a CSPModule, and the per-layer ops [alt0, alt1) it replaces at shapes where it fits
     int ck[7] = {-1, -1, -1, -1, -1, -1, -1};
     int alt0 = -1, alt1 = -1;
+    // OP_BOXCHAIN: per level the box.l.0 / box.l.1 / box.l.2 convs (input hx[l]), the per-layer
+    // ops it replaces at shapes where every level has a tile (bops: box.l.0 per level first)
+    int bxc[3][3] = {{-1, -1, -1}, {-1, -1, -1}, {-1, -1, -1}};
+    std::vector<int> alts;
     std::string label;
 };
 
@@ -168,11 +174,12 @@ struct GraphKey {
 // YH_C3K=0 keeps the C3k blocks as per-layer launches (compared bit for bit by the tests),
 // YH_HCLS_WIDE=0 keeps a 256-channel level's cls branch (v11_n 20x20) as per-layer launches.
 struct Options {
-    bool fuse = true, csp_tail = false, tune_log = false, c3k = true, hcls_wide = true;
+    bool fuse = true, csp_tail = false, tune_log = false, c3k = true, hcls_wide = true, box_chain = false;
     int conv_force = -1;
     static Options from_env() {
         Options o;
         if (const char* e = getenv("YH_FUSE")) o.fuse = atoi(e) != 0;
+        if (const char* e = getenv("YH_BOXCHAIN")) o.box_chain = atoi(e) != 0;
         if (const char* e = getenv("YH_CSP_TAIL")) o.csp_tail = atoi(e) != 0;
         if (const char* e = getenv("YH_C3K")) o.c3k = atoi(e) != 0;
         if (const char* e = getenv("YH_HCLS_WIDE")) o.hcls_wide = atoi(e) != 0;
@@ -494,11 +501,14 @@ struct Net {
         Op bdop;
         bdop.kind = OP_BOXDFL;
         bdop.label = "head.box_dfl";
+        int bop[3][2];   // per level: the ops of box.l.0 and box.l.1
         for (int l : {2, 1, 0}) {
             const int lvl = 3 + l;
             const std::string bp = "head.box." + std::to_string(l);
             const int tb1 = tensor(lvl, boxc), tb2 = tensor(lvl, boxc);
+            bop[l][0] = (int)ops.size();
             conv3(bp + ".0", full(xs[l], xc[l]), xc[l], boxc, 1, ACT_SILU, full(tb1, boxc));
+            bop[l][1] = (int)ops.size();
             conv3(bp + ".1", full(tb1, boxc), boxc, boxc, 1, ACT_SILU, full(tb2, boxc));
             if (fdec) {
                 bdop.bc[l] = new_dense_conv(bp + ".2", boxc, 64, 1, 1, ACT_ID);
@@ -532,6 +542,23 @@ struct Net {
         }
         if (fuse_any) ops.push_back(hcop);
         if (fdec) ops.push_back(bdop);
+        // 16-bit handles: the whole box branch of every level as one launch (boxc.hip) at shapes
+        // where each level has a tile (ensure_plan picks it or the seven launches above)
+        if (fdec && fuse_box_chain(boxc, xs, xc)) {
+            Op bc;
+            bc.kind = OP_BOXCHAIN;
+            bc.label = "head.box";
+            for (int l = 0; l < 3; ++l) {
+                bc.bxc[l][0] = ops[bop[l][0]].conv;
+                bc.bxc[l][1] = ops[bop[l][1]].conv;
+                bc.bxc[l][2] = bdop.bc[l];
+                bc.hx[l] = full(xs[l], xc[l]);
+            }
+            for (int l = 0; l < 3; ++l) bc.alts.push_back(bop[l][0]);
+            for (int l = 0; l < 3; ++l) bc.alts.push_back(bop[l][1]);
+            bc.alts.push_back((int)ops.size() - 1);   // box_dfl
+            ops.push_back(bc);
+        }
         Op dec;
         dec.kind = OP_DECODE;
         for (int l = 0; l < 3; ++l) dec.lvl[l] = full(L[l]);
@@ -745,6 +772,102 @@ struct Net {
         d0.mx_w.emplace("c3k", dev);
         for (int k = 1; k < 7; ++k) convs[op.ck[k]].mx_w.emplace("c3k_dep", nullptr);
         return dev;
+    }
+    // the box branch runs as one launch (boxc.hip) for 64 box channels and level inputs of
+    // 64 / 128 / 256 / 512 channels (plain views)
+    bool fuse_box_chain(int boxc, const int (&xs)[3], const int (&xc)[3]) const {
+        if (dtype == F32 || !opt.fuse || !opt.box_chain || boxc != 64) return false;
+        for (int l = 0; l < 3; ++l)
+            if (!bx_ok(xc[l]) || tensors[xs[l]].C != xc[l]) return false;
+        return true;
+    }
+    // packed parameters of one level of the box chain (boxc.hip layout), cached with box.l.0
+    const void* box_chain_params(const Op& op, int l) {
+        ConvDesc& d0 = convs[op.bxc[l][0]];
+        auto it = d0.mx_w.find("bxc");
+        bool ok = it != d0.mx_w.end();
+        for (int k = 1; k < 3; ++k) ok = ok && convs[op.bxc[l][k]].mx_w.count("bxc_dep");
+        if (ok) return it->second;
+        if (it != d0.mx_w.end()) {
+            (void)hipFree(it->second);
+            d0.mx_w.erase(it);
+        }
+        for (int k = 0; k < 3; ++k) require(convs[op.bxc[l][k]].loaded, "weights of " + convs[op.bxc[l][k]].name + " not loaded", YH_ESTATE);
+        const ConvDesc &c0 = convs[op.bxc[l][0]], &c1 = convs[op.bxc[l][1]], &c2 = convs[op.bxc[l][2]];
+        const int C0 = c0.cin, ncb = C0 / 16;
+        require(c0.cout == 64 && c1.cin == 64 && c1.cout == 64 && c2.cin == 64 && c2.cout == 64 && c2.k == 1,
+                "box chain: conv shapes");
+        std::vector<uint8_t> img((size_t)bx_prm_bytes(C0), 0);
+        uint16_t* dst = reinterpret_cast<uint16_t*>(img.data());
+        auto cvt = [&](float v) { return dtype == BF16 ? f2bf(v) : f2h(v); };
+        const size_t item = 18 * 1024 / 2;   // ring item (uint16 units)
+        for (int lane = 0; lane < 64; ++lane) {
+            const int R = lane & 31, hh = lane >> 5;
+            for (int a = 0; a < 2; ++a) {
+                // conv_mx's rows (lane half hh: couts 16 hh ..) and c3k's permuted rows (registers
+                // 8 jj .. of tile a = channels 32 a + 16 jj + 8 hh ..: the 1x1's B fragments)
+                const int co0 = 32 * a + 16 * ((R >> 2) & 1) + (R & 3) + 4 * (R >> 3);
+                const int co1 = 32 * a + ((R & 0x13) | ((R & 4) << 1) | ((R & 8) >> 1));
+                const int co2 = 32 * ((R >> 2) & 1) + 16 * a + (R & 3) + 4 * (R >> 3);   // box_dfl's rows
+                for (int j = 0; j < 8; ++j) {
+                    for (int cb = 0; cb < ncb; ++cb)
+                        for (int t = 0; t < 9; ++t)
+                            dst[cb * item + ((size_t)(a * 9 + t) * 64 + lane) * 8 + j] =
+                                cvt(c0.wf[((size_t)co0 * C0 + 16 * cb + 8 * hh + j) * 9 + t]);
+                    for (int kb = 0; kb < 4; ++kb) {
+                        for (int t = 0; t < 9; ++t)
+                            dst[(ncb + kb) * item + ((size_t)(a * 9 + t) * 64 + lane) * 8 + j] =
+                                cvt(c1.wf[((size_t)co1 * 64 + 16 * kb + 8 * hh + j) * 9 + t]);
+                        dst[(ncb + 4) * item + ((size_t)(a * 4 + kb) * 64 + lane) * 8 + j] =
+                            cvt(c2.wf[(size_t)co2 * 64 + 16 * kb + 8 * hh + j]);
+                    }
+                }
+            }
+        }
+        float* bd = reinterpret_cast<float*>(img.data() + img.size() - 3 * 64 * 4);
+        for (int i = 0; i < 64; ++i) {
+            bd[i] = c0.bf[i];
+            bd[64 + i] = c1.bf[i];
+            bd[128 + i] = c2.bf[i];
+        }
+        void* dev = nullptr;
+        HIPCHECK(hipMalloc(&dev, img.size()));
+        HIPCHECK(hipMemcpy(dev, img.data(), img.size(), hipMemcpyHostToDevice));
+        d0.mx_w.emplace("bxc", dev);
+        for (int k = 1; k < 3; ++k) convs[op.bxc[l][k]].mx_w.emplace("bxc_dep", nullptr);
+        return dev;
+    }
+    BoxChainArgs box_chain_args(const Op& op, int B, int H, int W) {
+        BoxChainArgs a{};
+        a.B = B;
+        a.nc = var.num_classes;
+        a.A = anchor_off(3, H, W);
+        a.io = (const void* const*)io_dev;
+        a.zero = zero_dev;
+        int wg = 0;
+        for (int l = 0; l < 3; ++l) {
+            BoxChainLevel& v = a.lv[a.nlv++];
+            const int lv = tensors[op.hx[l].t].level;
+            v.x = ptr(op.hx[l]);
+            v.ldx = ldc(op.hx[l]);
+            v.C0 = convs[op.bxc[l][0]].cin;
+            v.H = H >> lv;
+            v.W = W >> lv;
+            require(bx_tile(v.H, v.W, v.TH, v.TW), "head.box: no tile");
+            v.ntw = (v.W + v.TW - 1) / v.TW;
+            v.tiles = v.ntw * ((v.H + v.TH - 1) / v.TH);
+            // box.l.0's canonical K order at this shape (conv_mx.h mx_kchunks)
+            ConvArgs ca{};
+            int BM, BN;
+            conv_args(ops[op.alts[l]], B, H, W, ca, BM, BN);
+            v.nkc = mx_kchunks(mx_shape(ca, B));
+            v.stride = (float)(1 << lv);
+            v.aoff = anchor_off(l, H, W);
+            v.prm = box_chain_params(op, l);
+            v.wg0 = wg;
+            wg += B * v.tiles;
+        }
+        return a;
     }
     // the decode folds into box_dfl + head_cls / a class-rows decode (16-bit handles; the
     // box branch's last conv has 4 or 6 16-channel K blocks)
@@ -1336,6 +1459,7 @@ struct Net {
                 break;
             }
             case OP_BOXDFL: rc = launch_box_dfl(dtype, box_dfl_args(op, B, H, W), s); break;
+            case OP_BOXCHAIN: rc = launch_box_chain(dtype, box_chain_args(op, B, H, W), s); break;
             case OP_STEM2: {
                 const ConvDesc& d = convs[op.conv];
                 Stem2Args a{};
@@ -1417,6 +1541,19 @@ struct Net {
         // a fused C3k block runs where bands of its map fit a workgroup's LDS (c3k_lds), its
         // seven per-layer launches everywhere else
         pl.active.assign(ops.size(), 1);
+        for (size_t i = 0; i < ops.size(); ++i) {
+            if (ops[i].kind != OP_BOXCHAIN) continue;
+            bool fits = true;
+            for (int l = 0; l < 3; ++l) {
+                const int lv = tensors[ops[i].hx[l].t].level;
+                int th, tw;
+                fits = fits && bx_tile(H >> lv, W >> lv, th, tw);
+            }
+            if (fits)
+                for (int k : ops[i].alts) pl.active[k] = 0;
+            else
+                pl.active[i] = 0;
+        }
         for (size_t i = 0; i < ops.size(); ++i) {
             if (ops[i].kind != OP_C3K) continue;
             const int lv = tensors[ops[i].out.t].level;
@@ -1520,6 +1657,7 @@ struct Net {
             case OP_CSP: return CL_CSP;
             case OP_STEM2: return CL_FIRST;
             case OP_C3K: return CL_C3K;
+            case OP_BOXCHAIN: return CL_BOXCHAIN;
         }
         return CL_CONV1;
     }
@@ -1635,6 +1773,17 @@ struct Net {
                 }
                 break;
             }
+            case OP_BOXCHAIN: {
+                // the level inputs read once, 4 box rows written, the three convs' weights once
+                for (int l = 0; l < 3; ++l) {
+                    const double n = px(tensors[op.hx[l].t].level);
+                    const int C0 = convs[op.bxc[l][0]].cin;
+                    const double macs = 64.0 * C0 * 9 + 64.0 * 64 * 9 + 64.0 * 64;
+                    bytes += n * C0 * es + n * 4 * es + macs * es + 3 * 64 * 4.0;
+                    flops += 2.0 * n * macs + n * 64 * 4.0;
+                }
+                break;
+            }
             case OP_BOXDFL: {
                 // the box.l.1 outputs read once, 4 box rows written, weights once per level
                 for (int l = 0; l < 3; ++l) {
@@ -1691,6 +1840,9 @@ struct Net {
             case OP_BOXDFL:
                 for (int l = 0; l < 3; ++l) add("x" + std::to_string(l), op.bx[l], 0, op.bx[l].C);
                 break;
+            case OP_BOXCHAIN:
+                for (int l = 0; l < 3; ++l) add("x" + std::to_string(l), op.hx[l], 0, op.hx[l].C);
+                break;
             case OP_DECODE:
                 for (int l = 0; l < 3; ++l) add("L" + std::to_string(l), op.lvl[l], 0, 64 + var.num_classes);
                 break;
@@ -1711,6 +1863,12 @@ struct Net {
                 return r;
             }
             case OP_BOXDFL: return {op.bc[0], op.bc[1], op.bc[2]};
+            case OP_BOXCHAIN: {
+                std::vector<int> r;
+                for (int l = 0; l < 3; ++l)
+                    for (int k = 0; k < 3; ++k) r.push_back(op.bxc[l][k]);
+                return r;
+            }
             case OP_SPPF: case OP_DECODE: return {};
         }
         return {};
