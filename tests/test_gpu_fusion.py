@@ -267,14 +267,14 @@ def test_c3k_row_bands_equal_per_layer_launches(gpu, bands):
                                                      ("n", torch.bfloat16, 2, 608, 480), ("n", torch.bfloat16, 1, 1280, 1280),
                                                      ("s", torch.float16, 2, 384, 640), ("m", torch.bfloat16, 1, 320, 320)])
 def test_box_chain_equals_per_layer_launches(gpu, variant, dtype, batch, h, w):
-    """boxc.hip: the box branch of all three levels (box.l.0 3x3 -> box.l.1 3x3 -> box.l.2 1x1 + DFL
-    + anchors + dist2bbox) in one launch, the 64-channel intermediates in LDS, is bit-identical to the
-    seven per-layer launches (YH_BOXCHAIN=0): whole and partial tiles, level inputs of 64 / 128 / 256
+    """boxc.hip (opt-in, YH_BOXCHAIN=1): the box branch of all three levels (box.l.0 3x3 -> box.l.1 3x3
+    -> box.l.2 1x1 + DFL + anchors + dist2bbox) in one launch, the 64-channel intermediates in LDS, is
+    bit-identical to the seven per-layer launches (YH_BOXCHAIN=0): whole and partial tiles, level inputs of 64 / 128 / 256
     (n) and 128 / 256 / 512 (s) channels, K-split (mx_kchunks: 640, 40x40 / 20x20 levels) and
     unsplit box.l.0 shapes (1280: 80x80 / 40x40), an anchor count that is not a multiple of 8."""
     model = make_model(variant)
     x = synth.synth_scenes(batch, h, w, seed=43).to(gpu, dtype)
-    fused = _engine(model, dtype, gpu, True)
+    fused = _engine(model, dtype, gpu, True, YH_BOXCHAIN="1")   # opt-in (slower than the per-layer launches)
     plain = _engine(model, dtype, gpu, True, YH_BOXCHAIN="0")
     yf = fused.forward(x).clone()
     yp = plain.forward(x).clone()

@@ -19,7 +19,8 @@ Covered kernels (by configuration):
   * C2 v11_n bf16 640 b32 (images 0, 17, 31): the tuned conv_mx / conv_mxr / conv_rw plans incl.
     the K-split ones (20x20 / 40x40 layers), stem_fused, csp_fused (whole-block and tail mode),
     c3k_fused in row bands and in SPLIT mode, sppf_fused, psa_attention_full, head_cls (all three
-    levels, scores written straight into y), box_chain (the whole box branch of the three levels);
+    levels, scores written straight into y), box_dfl; with YH_BOXCHAIN=1 (n bf16 b2) the opt-in
+    fused box branch of the three levels (boxc.hip);
   * v11_n fp16 640 b2: the same kernels in fp16;
   * C3 v11_s fp16 640 b64 (images 0, 63): wider conv plans, seven-launch C3k, per-layer cls
     branches (dwconv3x3_c4) and the class-rows decode (head_decode_lds);
@@ -203,20 +204,27 @@ def run_op_parity(gpu, variant, dtype, batch, size, images, seed):
 
 def test_op_parity_c2_n_bf16_b32(gpu):
     kinds, n = run_op_parity(gpu, "n", torch.bfloat16, 32, 640, (0, 17, 31), seed=21)
-    assert {"stem_fused", "conv", "c3k2", "c3k", "sppf", "attention", "head_cls", "box_chain"} <= kinds, kinds
+    assert {"stem_fused", "conv", "c3k2", "c3k", "sppf", "attention", "head_cls", "box_dfl"} <= kinds, kinds
 
 
 def test_op_parity_n_fp16(gpu):
     kinds, n = run_op_parity(gpu, "n", torch.float16, 2, 640, (0, 1), seed=22)
-    assert {"stem_fused", "conv", "c3k2", "c3k", "sppf", "attention", "head_cls", "box_chain"} <= kinds, kinds
+    assert {"stem_fused", "conv", "c3k2", "c3k", "sppf", "attention", "head_cls", "box_dfl"} <= kinds, kinds
 
 
 def test_op_parity_c3_s_fp16_b64(gpu):
     kinds, n = run_op_parity(gpu, "s", torch.float16, 64, 640, (0, 63), seed=23)
-    assert {"stem_fused", "conv", "c3k2", "dwconv", "decode", "box_chain", "attention", "sppf"} <= kinds, kinds
+    assert {"stem_fused", "conv", "c3k2", "dwconv", "decode", "box_dfl", "attention", "sppf"} <= kinds, kinds
 
 
 def test_op_parity_c5_x_bf16_1280(gpu):
     kinds, n = run_op_parity(gpu, "x", torch.bfloat16, 1, 1280, (0,), seed=24)
     assert {"stem", "conv", "dwconv", "decode", "box_dfl", "attention", "sppf"} <= kinds, kinds
     # (x: 96 box channels, the per-layer box convs + box_dfl)
+
+
+def test_op_parity_box_chain_n_bf16(gpu, monkeypatch):
+    """The opt-in fused box branch (boxc.hip, YH_BOXCHAIN=1 at handle creation) op by op."""
+    monkeypatch.setenv("YH_BOXCHAIN", "1")
+    kinds, n = run_op_parity(gpu, "n", torch.bfloat16, 2, 640, (0, 1), seed=25)
+    assert "box_chain" in kinds, kinds

@@ -236,7 +236,7 @@ int main(int argc, char** argv) {
                 }
             }
             printf("  %s na%d mb%d wn%d wm%d ncb%d  task %dx%d bc%d nbi%d ains%d lds%6d grid%5d conf%4d | %8.2f us %7.0f GB/s %6.0f TF | maxd %.3g bad %lld %s\n",
-                   pl.cfg.kind == 2 ? (pl.cfg.nbuf == 2 ? "W2" : pl.cfg.nbuf == 3 ? "W3" : "W4") : pl.cfg.kind ? "R" : "S", pl.cfg.na, pl.cfg.mb, pl.cfg.wn, pl.cfg.wm, pl.cfg.ncb, pl.TH, pl.TW, 1 << pl.bc_log2, pl.nbi, pl.ains,
+                   pl.cfg.kind == 2 ? (pl.cfg.pc ? (pl.cfg.nbuf == 3 ? "C3" : pl.cfg.nbuf == 4 ? "C4" : "C5") : pl.cfg.nbuf == 2 ? "W2" : pl.cfg.nbuf == 3 ? "W3" : pl.cfg.nbuf == 4 ? "W4" : "W5") : pl.cfg.kind ? "R" : "S", pl.cfg.na, pl.cfg.mb, pl.cfg.wn, pl.cfg.wm, pl.cfg.ncb, pl.TH, pl.TW, 1 << pl.bc_log2, pl.nbi, pl.ains,
                    pl.lds, pl.grid, pl.conflicts, us, bytes / us * 1e-3, flops / us * 1e-6, maxd, bad,
                    ident ? "ident" : "DIFF");
             if (getenv("MX_TRACE")) {

@@ -35,7 +35,10 @@ constexpr int BX_NW = 8;                  // waves per workgroup
 constexpr int BX_THREADS = 64 * BX_NW;
 constexpr int BX_ITEM = 18 * 1024;        // ring item: both 32-cout tiles x 9 taps of one K block
 constexpr int BX_PPW = 3;                 // 1-KB DMA pieces per wave and item (8 x 3 >= 18)
-constexpr int BX_NB = 2;                  // ring buffers
+#ifndef BX_NB_DEF
+#define BX_NB_DEF 2
+#endif
+constexpr int BX_NB = BX_NB_DEF;          // ring buffers (2 / 3 / 5 measured alike: 142-157 us)
 
 template <typename T> struct BMfma;
 template <> struct BMfma<__bf16> {
@@ -69,6 +72,17 @@ __device__ __forceinline__ void bx_glds(const void* src, unsigned lds_addr) {
 #endif
 }
 __device__ __forceinline__ void bx_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+// wait until at most k ring items (BX_PPW = 3 DMA instructions each) of this wave are in flight
+__device__ __forceinline__ void bx_wait_items(int k) {
+    switch (k) {
+        case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+        case 1: asm volatile("s_waitcnt vmcnt(3)" ::: "memory"); break;
+        case 2: asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); break;
+        case 3: asm volatile("s_waitcnt vmcnt(9)" ::: "memory"); break;
+        case 4: asm volatile("s_waitcnt vmcnt(12)" ::: "memory"); break;
+        default: asm volatile("s_waitcnt vmcnt(15)" ::: "memory"); break;
+    }
+}
 // byte offset of 16-B chunk c of pixel p in a 64-channel (8-chunk) image, chunks swizzled by
 // the pixel so a ds_read_b128 lane group of consecutive pixels spreads over the banks
 __device__ __forceinline__ int bx_off(int p, int c) { return p * 128 + ((c ^ ((p >> 1) & 7)) << 4); }
@@ -191,11 +205,10 @@ __device__ __forceinline__ void bx_body(const BoxChainArgs& A, int li, char* sm)
     //      piece's tail), the first ring item
     load_x(0);
     if (wv == 0)
-        bx_glds(lane < 48 ? (const void*)(prm + bx_prm_off_b(NCB0) + lane * 16) : A.zero, lds0 + (unsigned)(dummy_off + 1024));
+        bx_glds(lane < 48 ? (const void*)(prm + bx_prm_off_b(NCB0 * 16) + lane * 16) : A.zero, lds0 + (unsigned)(dummy_off + 1024));
     for (int i = 0; i < BX_NB - 1; ++i) issue(i);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     bx_barrier();
-
     // ---- units: wave wv owns M pixels [32 wv, 32 wv + 32) (box.l.0) and tile pixels
     //      [32 wv, ...) (box.l.1 / the 1x1); lanes past the region compute clamped pixels
     const bool own0 = wv * 32 < NM, own1 = wv * 32 < NT;   // wave-uniform
@@ -213,9 +226,9 @@ __device__ __forceinline__ void bx_body(const BoxChainArgs& A, int li, char* sm)
 
 #pragma unroll 1
     for (int i = 0; i < NITEMS; ++i) {
-        // this wave's pieces of item i landed (with two buffers: everything it issued), then
+        // this wave's pieces of item i landed (items i + 1 .. i + NB - 2 may stay in flight), then
         // everyone's; step i - 1 is done everywhere
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        bx_wait_items(min(i + BX_NB - 1, NITEMS) - (i + 1));
         bx_barrier();
         issue(i + BX_NB - 1);
         const char* wb = sm + ring_off + (i % BX_NB) * BX_ITEM;
@@ -364,14 +377,14 @@ __global__ __launch_bounds__(BX_THREADS, 2) void box_chain(const BoxChainArgs A)
 }  // namespace
 
 // output tile of a level: the largest candidate with <= 8 units of 32 pixels in both convs
-// (tile + 1-pixel halo, and the tile), the least padding waste first, within 80 KB of LDS
+// (tile + 1-pixel halo, and the tile), the least padding waste first, within the 160 KB of LDS
 bool bx_tile(int H, int W, int& TH, int& TW) {
     static const int cand[][2] = {{12, 16}, {8, 20}, {8, 16}, {5, 20}, {10, 10}, {8, 8}, {4, 16}, {4, 8}, {4, 4}, {2, 4}};
     double best = 1e30;
     bool found = false;
     for (auto& c : cand) {
         const int th = std::min(c[0], H), tw = std::min(c[1], W);
-        if ((th + 2) * (tw + 2) > 256 || th * tw > 256 || bx_lds_bytes(th, tw) > 80 * 1024) continue;
+        if ((th + 2) * (tw + 2) > 256 || th * tw > 256 || bx_lds_bytes(th, tw) > 160 * 1024) continue;
         // cost per output: padded tiles' box.l.0 units (halo) + box.l.1 units
         const int ntw = (W + tw - 1) / tw, nth = (H + th - 1) / th;
         const double units = (double)ntw * nth * (((th + 2) * (tw + 2) + 31) / 32 * 2.0 + (th * tw + 31) / 32);

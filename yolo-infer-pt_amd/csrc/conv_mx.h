@@ -65,6 +65,7 @@ struct MxArgs {
     FastDiv d_wo, d_howo;               // KS == 1: flat pixel -> (n, ho, wo)
     FastDiv d_ntw, d_nth, d_nsl;        // task id decomposition
     int M;                              // B * Ho * Wo
+    int pc_delay;                       // conv_rw counter mode: s_sleep(32) rounds of the late half
 #ifdef YH_ABLATION
     // tools/micro builds only (-DYH_ABLATION; the shipped library has neither field):
     int dbg;                            // 1 no weight DMA, 2 no patch DMA, 4 no MFMA, 8 no epilogue
@@ -89,6 +90,9 @@ struct MxConfig {
     int tw = 0;       // conv_rw: output tile width (template)
     int gdiv = 1;     // conv_rw: workgroups = (one per CU share) / gdiv (fewer weight-image loads)
     int nkc = 1;      // conv_rw: 64-channel K chunks, one wave each (mx_kchunks of the layer)
+    int pc = 0;       // conv_rw: 1 = no per-tile workgroup barrier: slot hand-offs through LDS
+                      //    counters, tiles issued nbuf - 2 ahead, the second half of the waves
+                      //    started half a tile late (conv_rw.hip, "counter mode")
     int bn() const { return 32 * na * wn; }
     int nw() const { return wn * wm; }
 };

@@ -29,6 +29,7 @@
 #include "dtypes.h"
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 
 #ifndef RW_PF
@@ -55,8 +56,9 @@ RwGeo rw_geo(int S, int cin, int ncg, int npg, int mb, int tw, bool res, int nkc
     g.nbr = res ? (g.tpx * ncg * 4 + 64 * g.nw - 1) / (64 * g.nw) : 0;
     g.slot = (g.nbi + g.nbr) * g.nw * 1024;
     g.red = (nkc - 1) * ncg * npg * mb * 4096;
-    // coalesced epilogue: one 32-pixel x 32-cout staging tile per storing wave, + the slice's bias
-    g.epi = ncg * npg * 2048 + ncg * 128;
+    // coalesced epilogue: one 32-pixel x 32-cout staging tile per storing wave, + the slice's bias,
+    // + the counter mode's slot counters (2 x 8 words)
+    g.epi = ncg * npg * 2048 + ncg * 128 + 64;
     return g;
 }
 
@@ -97,6 +99,19 @@ __device__ __forceinline__ void rw_barrier() {
     __builtin_amdgcn_s_barrier();
 }
 
+// counter mode: wait (bounded) until the LDS word at p reaches target; bump it (one lane)
+__device__ __forceinline__ void rw_spin(const unsigned* p, unsigned target) {
+    for (int k = 0; k < (1 << 22); ++k) {
+        const unsigned v = __builtin_amdgcn_readfirstlane(*reinterpret_cast<const volatile unsigned*>(p));
+        if (v >= target) break;
+        __builtin_amdgcn_s_sleep(1);
+    }
+}
+__device__ __forceinline__ void rw_signal(unsigned* p, int lane) {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // this wave's LDS reads of the slot are done
+    if (lane == 0) __hip_atomic_fetch_add(p, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
 __device__ __forceinline__ uint32_t rw_fdiv(uint32_t x, FastDiv d) {
     return (uint32_t)(((uint64_t)__umulhi(x, d.m) + x) >> d.s);
 }
@@ -133,7 +148,13 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t rw_rsrc(const void* base) {
 
 }  // namespace
 
-template <typename T, int S, int CIN, int NCG, int NPG, int MB, int TW, int NS, bool RES, int NKC>
+// CM (counter mode, NKC = 1): no workgroup barrier per tile. Tile it + NS - 2 is issued at
+// iteration it into the slot tile it - 2 used, once every wave has signalled it done with that
+// tile (LDS counter); a wave starts tile it once every wave has signalled its pieces of tile it
+// landed. Waves may drift up to a tile apart: the second half of the waves starts half a tile
+// late, so on each SIMD one wave's epilogue (VALU: SiLU, the staging, the stores) runs beside
+// the other's MFMAs instead of after them. Same arithmetic, same bits.
+template <typename T, int S, int CIN, int NCG, int NPG, int MB, int TW, int NS, bool RES, int NKC, bool CM>
 __global__ __launch_bounds__(64 * NCG * NKC * NPG, (NCG * NKC * NPG >= 8 || NCG > 1 || CIN <= 32) ? 2 : 1) void conv_rw(
     const MxArgs p) {
     constexpr int NW = NCG * NKC * NPG;
@@ -157,6 +178,11 @@ __global__ __launch_bounds__(64 * NCG * NKC * NPG, (NCG * NKC * NPG >= 8 || NCG 
     constexpr int CNT0 = (NS - 1) * 2 * MB + (NS - 2) * (NBI + NBR);
     constexpr int CNT1 = (NS - 2) * (NBI + NBR);
     static_assert(CNT0 <= 63, "vmcnt range");
+    // counter mode: tiles issued D = NS - 2 ahead; at the wait for tile it's DMA, the wave has
+    // issued since then the DMAs of D - 1 tiles and the stores of D epilogues
+    constexpr int DPC = NS - 2;
+    constexpr int CNTP = DPC * 2 * MB + (DPC - 1) * (NBI + NBR);
+    static_assert(!CM || (NKC == 1 && NS >= 3 && CNTP <= 63), "counter mode geometry");
 
     const unsigned long long t_entry = RW_TRACE ? __builtin_amdgcn_s_memrealtime() : 0ull;
     extern __shared__ __attribute__((aligned(1024))) uint4 sm4[];
@@ -304,6 +330,9 @@ __global__ __launch_bounds__(64 * NCG * NKC * NPG, (NCG * NKC * NPG >= 8 || NCG 
     // where its vmcnt(0) would drain the patch ring every iteration)
 #pragma unroll
     for (int s = 0; s < NKS; ++s) asm volatile("" :: "v"(wf[s].x), "v"(wf[s].y), "v"(wf[s].z), "v"(wf[s].w));
+    // counter mode: landed[NS] then done[NS], zeroed before the barrier below
+    unsigned* cnt = reinterpret_cast<unsigned*>(reinterpret_cast<char*>(sm4) + NS * SLOT + RED + NCG * NPG * 2048 + NCG * 128);
+    if (CM && (int)threadIdx.x < 2 * NS) cnt[threadIdx.x] = 0u;
     rw_vmwait<0>();
     rw_barrier();
     const unsigned long long t_setup = RW_TRACE ? __builtin_amdgcn_s_memrealtime() : 0ull;
@@ -371,8 +400,32 @@ __global__ __launch_bounds__(64 * NCG * NKC * NPG, (NCG * NKC * NPG >= 8 || NCG 
         }
     };
     unsigned long long t_wait = 0ull;   // diagnostic builds, dbg 64: time spent in the loop-top waits
+    if constexpr (CM) {
+        // the prologue issued tiles 0 .. NS - 2; tiles 0 .. DPC - 1 are the ones this loop expects
+        // (issue distance DPC): the remaining one (NS - 2) is also in flight, counted like the rest
+        if (wv >= NW / 2) {   // the second half of the waves starts half a tile late
+#pragma unroll 1
+            for (int k = 0; k < p.pc_delay; ++k) __builtin_amdgcn_s_sleep(32);
+        }
+    }
     for (int it = 0; it < n_it; ++it) {
-        if (it > 0) {
+        if constexpr (CM) {
+            const int sl_it = it % NS;
+            if (it >= NS - 1) {
+                // tiles past the prologue's: this wave's pieces landed, then everyone's (the count
+                // of slot sl_it's tiles from NS - 1 on, this one included)
+                const int first = sl_it == NS - 1 ? NS - 1 : sl_it + NS;
+                rw_vmwait<CNTP>();
+                rw_signal(cnt + sl_it, lane);
+                rw_spin(cnt + sl_it, (unsigned)(NW * ((it - first) / NS + 1)));
+            }
+            if (it >= 1) {
+                // tile it + NS - 2 into the slot tile it - 2 used, once every wave is done with it
+                // (tile NS - 1, issued at it = 1, takes the ring's unused last slot)
+                if (it >= 2) rw_spin(cnt + NS + (it - 2) % NS, (unsigned)(NW * ((it - 2) / NS + 1)));
+                issue(it + NS - 2, (it + NS - 2) % NS);
+            }
+        } else if (it > 0) {
             const unsigned long long tw0 = (RW_TRACE && RW_DBG(64)) ? __builtin_amdgcn_s_memrealtime() : 0ull;
             if (kc == 0) rw_vmwait<CNT0>();
             else rw_vmwait<CNT1>();
@@ -380,7 +433,7 @@ __global__ __launch_bounds__(64 * NCG * NKC * NPG, (NCG * NKC * NPG >= 8 || NCG 
             if (RW_TRACE && RW_DBG(64)) t_wait += __builtin_amdgcn_s_memrealtime() - tw0;
             if (RW_TRACE && it == 1) t_first = __builtin_amdgcn_s_memrealtime();
         }
-        issue(it + NS - 1, (it + NS - 1) % NS);
+        if constexpr (!CM) issue(it + NS - 1, (it + NS - 1) % NS);
 
         // ---- MFMAs: one k-step = one 32x32x16 step per B tile, fragments of step s+1
         //      read while step s multiplies
@@ -438,7 +491,7 @@ __global__ __launch_bounds__(64 * NCG * NKC * NPG, (NCG * NKC * NPG >= 8 || NCG 
             }
         }
         if (kc == 0) epilogue(it);
-
+        if constexpr (CM) rw_signal(cnt + NS + it % NS, lane);
     }
     if (RW_TRACE && threadIdx.x == 0) {
         unsigned long long* tr = RW_TRACE + blockIdx.x * 4;
@@ -543,10 +596,10 @@ void mx_candidates_w(const MxShape& sh, std::vector<MxConfig>& out) {
     if (!(sh.cin == 16 || sh.cin == 32 || sh.cin == 64 || nkc > 1)) return;
     // small layers (fewer tiles than 2 per CU) also get the grid halved and quartered
     const bool small = (double)sh.B * sh.Ho * sh.Wo < 2.0 * 256 * 64;
-    auto add = [&](int ncg, int npg, int mb, int tw, int ns) {
+    auto add = [&](int ncg, int npg, int mb, int tw, int ns, int pc = 0) {
         MxConfig c{};
         c.kind = 2; c.ks = 3; c.s = sh.s; c.na = ncg; c.mb = mb; c.wn = ncg; c.wm = npg; c.ncb = sh.cin / 16;
-        c.tw = tw; c.nbuf = ns; c.nkc = nkc;
+        c.tw = tw; c.nbuf = ns; c.nkc = nkc; c.pc = pc;
         for (int gd : {1, 2, 4}) {
             if (gd > 1 && !small) break;
             c.gdiv = gd;
@@ -568,6 +621,9 @@ void mx_candidates_w(const MxShape& sh, std::vector<MxConfig>& out) {
     } else if (sh.s == 1) {
         if (sh.cin == 64 && ncg == 2) {
             add(2, 4, 1, 16, 4); add(2, 4, 1, 8, 4); add(2, 2, 1, 8, 4); add(2, 2, 1, 4, 4); add(2, 2, 1, 8, 3);
+            // counter mode (YH_RW_CM=1 only: bit-identical, measured slower, r05 micro bench box0.0:
+            // 26.8-27.5 us against 25.5 us for the barrier ring)
+            if (getenv("YH_RW_CM")) { add(2, 4, 1, 16, 4, 1); add(2, 4, 1, 16, 5, 1); add(2, 4, 1, 8, 4, 1); }
         } else if (sh.cin == 64 && ncg == 1) {
             add(1, 8, 1, 16, 3); add(1, 4, 1, 8, 4);
         } else if (sh.cin == 32 && ncg == 1) {
@@ -577,6 +633,7 @@ void mx_candidates_w(const MxShape& sh, std::vector<MxConfig>& out) {
         }
     } else if (sh.cin == 64 && ncg == 2) {
         add(2, 2, 1, 8, 3); add(2, 4, 1, 16, 2);
+        if (getenv("YH_RW_CM")) add(2, 2, 1, 8, 3, 1);
         // 128 couts in one workgroup: the patch is read once, not once per 64-cout slice
         if (sh.cout % 128 == 0) { add(4, 2, 1, 8, 3); add(4, 1, 1, 8, 4); }
     }
@@ -618,12 +675,12 @@ std::vector<uint16_t> mx_pack_w(const MxPlan& pl, const MxShape& sh, const float
 
 namespace {
 
-template <typename T, int S, int CIN, int NCG, int NPG, int MB, int TW, int NS, bool RES, int NKC>
+template <typename T, int S, int CIN, int NCG, int NPG, int MB, int TW, int NS, bool RES, int NKC, bool CM = false>
 int launch_rw_t(const MxPlan& pl, const MxArgs& a, hipStream_t s) {
     const RwGeo g = rw_geo(S, CIN, NCG, NPG, MB, TW, RES, NKC);
     if (g.nbi != pl.nbi || NS * g.slot + g.red + g.epi != pl.lds || RES != (a.res != nullptr)) return (int)hipErrorInvalidValue;
     static bool attr = false;
-    auto k = &conv_rw<T, S, CIN, NCG, NPG, MB, TW, NS, RES, NKC>;
+    auto k = &conv_rw<T, S, CIN, NCG, NPG, MB, TW, NS, RES, NKC, CM>;
     if (!attr) {
         (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize,
                                   160 * 1024);
@@ -638,10 +695,22 @@ int launch_rw_cfg(const MxPlan& pl, const MxArgs& a, hipStream_t s) {
     const MxConfig& c = pl.cfg;
 #define YH_RW(S_, CIN_, NCG_, NPG_, MB_, TW_, NS_, NKC_)                                                    \
     if (c.s == S_ && c.ncb * 16 == CIN_ && c.na == NCG_ && c.wm == NPG_ && c.mb == MB_ && c.tw == TW_ &&     \
-        c.nbuf == NS_ && c.nkc == NKC_) {                                                                    \
+        c.nbuf == NS_ && c.nkc == NKC_ && c.pc == 0) {                                                       \
         if (S_ == 1 && a.res) return launch_rw_t<T, S_, CIN_, NCG_, NPG_, MB_, TW_, NS_, (S_ == 1), NKC_>(pl, a, s); \
         return launch_rw_t<T, S_, CIN_, NCG_, NPG_, MB_, TW_, NS_, false, NKC_>(pl, a, s);                     \
     }
+#define YH_RWP(S_, CIN_, NCG_, NPG_, MB_, TW_, NS_)                                                          \
+    if (c.s == S_ && c.ncb * 16 == CIN_ && c.na == NCG_ && c.wm == NPG_ && c.mb == MB_ && c.tw == TW_ &&     \
+        c.nbuf == NS_ && c.nkc == 1 && c.pc == 1) {                                                          \
+        if (S_ == 1 && a.res) return launch_rw_t<T, S_, CIN_, NCG_, NPG_, MB_, TW_, NS_, (S_ == 1), 1, true>(pl, a, s); \
+        return launch_rw_t<T, S_, CIN_, NCG_, NPG_, MB_, TW_, NS_, false, 1, true>(pl, a, s);                   \
+    }
+    // counter mode (pc = 1)
+    YH_RWP(1, 64, 2, 4, 1, 16, 4)
+    YH_RWP(1, 64, 2, 4, 1, 16, 5)
+    YH_RWP(1, 64, 2, 4, 1, 8, 4)
+    YH_RWP(2, 64, 2, 2, 1, 8, 3)
+#undef YH_RWP
     YH_RW(1, 64, 2, 4, 1, 16, 4, 1)
     YH_RW(1, 64, 2, 4, 1, 8, 4, 1)
     YH_RW(1, 64, 2, 2, 1, 8, 4, 1)
@@ -673,7 +742,12 @@ int launch_rw_cfg(const MxPlan& pl, const MxArgs& a, hipStream_t s) {
 
 }  // namespace
 
-int launch_rw(int dtype, const MxPlan& pl, const MxArgs& a, hipStream_t s) {
+int launch_rw(int dtype, const MxPlan& pl, const MxArgs& a0, hipStream_t s) {
+    MxArgs a = a0;
+    // counter mode: how long the second half of the waves starts late (YH_RW_DELAY, read per
+    // launch: s_sleep(32) rounds of 2048 cycles)
+    const char* e = getenv("YH_RW_DELAY");
+    a.pc_delay = e ? std::max(0, atoi(e)) : 1;
     if (dtype == BF16) return launch_rw_cfg<__bf16>(pl, a, s);
     if (dtype == F16) return launch_rw_cfg<_Float16>(pl, a, s);
     return (int)hipErrorInvalidValue;

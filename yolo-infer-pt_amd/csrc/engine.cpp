@@ -845,7 +845,9 @@ struct Net {
         a.io = (const void* const*)io_dev;
         a.zero = zero_dev;
         int wg = 0;
-        for (int l = 0; l < 3; ++l) {
+        // workgroup order: the coarsest level, whose tiles are the longest, first (142 vs 148 us)
+        for (int k = 0; k < 3; ++k) {
+            const int l = 2 - k;
             BoxChainLevel& v = a.lv[a.nlv++];
             const int lv = tensors[op.hx[l].t].level;
             v.x = ptr(op.hx[l]);
@@ -1171,8 +1173,8 @@ struct Net {
     static std::string mx_name(const MxPlan& p) {
         char b[96];
         if (p.cfg.kind == 2)
-            snprintf(b, sizeof(b), "rw_g%d_p%d_mb%d_ns%d_t%dx%d%s", p.cfg.na, p.cfg.wm, p.cfg.mb, p.cfg.nbuf, p.TH, p.TW,
-                     p.cfg.gdiv == 2 ? "_d2" : p.cfg.gdiv == 4 ? "_d4" : "");
+            snprintf(b, sizeof(b), "rw_g%d_p%d_mb%d_ns%d_t%dx%d%s%s", p.cfg.na, p.cfg.wm, p.cfg.mb, p.cfg.nbuf, p.TH, p.TW,
+                     p.cfg.gdiv == 2 ? "_d2" : p.cfg.gdiv == 4 ? "_d4" : "", p.cfg.pc ? "_cm" : "");
         else
             snprintf(b, sizeof(b), "%s_na%d_mb%d_w%dx%d_ncb%d_t%dx%d", p.cfg.kind ? "mxr" : "mx", p.cfg.na, p.cfg.mb,
                      p.cfg.wn, p.cfg.wm, p.cfg.ncb, p.TH, p.TW);
