@@ -60,6 +60,25 @@ __device__ __forceinline__ void hc_glds(const void* src, unsigned lds_addr) {
 // Workgroup barrier for LDS hand-offs only: __syncthreads() also waits for every global
 // load in flight (vmcnt(0)), which would drain the weight loads issued ahead of a phase.
 __device__ __forceinline__ void hc_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+#ifdef YH_HC_TRACE
+// experiments only (-DYH_HC_TRACE builds; the shipped library has none of this): per-workgroup
+// phase stamps, read back by yh_debug_hc_trace. Slots: 0 / 8 s_memrealtime at entry / exit,
+// 1 s_memtime at entry, 2..7 s_memtime after the input landed, dw1, pw1, dw2, pw2, pw3, 9 HW_ID
+// | XCC_ID << 32 | level << 40.
+constexpr int HC_TR = 10, HC_TR_WG = 8192;
+__device__ unsigned long long hc_trace_buf[HC_TR_WG * HC_TR];
+#define HC_STAMP(k, rt)                                                                                      \
+    do {                                                                                                     \
+        hc_barrier();                                                                                        \
+        if (threadIdx.x == 0 && blockIdx.x < HC_TR_WG)                                                       \
+            hc_trace_buf[(size_t)blockIdx.x * HC_TR + (k)] =                                                 \
+                (rt) ? __builtin_amdgcn_s_memrealtime() : __builtin_amdgcn_s_memtime();                     \
+    } while (0)
+#else
+#define HC_STAMP(k, rt) \
+    do {                \
+    } while (0)
+#endif
 constexpr int HC_CK = 64;    // input channels staged per pass (the first depthwise conv's chunk)
 #ifndef YH_HC_RB
 #define YH_HC_RB 4
@@ -69,7 +88,7 @@ constexpr int HC_RB = YH_HC_RB;   // output rows per depthwise item (register sl
 // LDS of one tile: region 1 = the input chunk (XH x XW x min(C0, HC_CK)), later the first /
 // second pointwise outputs; region 2 = the first / second depthwise outputs
 struct HcLayout {
-    int SX, SD, SM, r1, prm, total;   // prm: byte offset of the fp32 parameters (see hc_params)
+    int SX, SD, SM, r1, x2, prm, total;   // prm: byte offset of the fp32 parameters (see hc_params)
 };
 __host__ __device__ inline HcLayout hc_layout(int TH, int TW, int C0, int c3) {
     HcLayout L;
@@ -83,6 +102,13 @@ __host__ __device__ inline HcLayout hc_layout(int TH, int TW, int C0, int c3) {
     a = a > p2 ? a : p2;
     L.r1 = (a + 15) & ~15;
     L.prm = L.r1 + (((d1 > d2 ? d1 : d2) + 15) & ~15);
+    // levels with several 64-channel chunks: a second input buffer (chunk k + 1 lands during
+    // chunk k's depthwise conv)
+    L.x2 = 0;
+    if (C0 > HC_CK) {
+        L.x2 = L.prm;
+        L.prm += x;
+    }
     // dw1 weights [9][C0] + bias, dw2 weights [9][c3] + bias, pw1 / pw2 / pw3 bias (HC_NA * 32 each)
     L.total = L.prm + (((10 * C0 + 10 * c3 + 3 * 96) * 4 + 1023) & ~1023);
     return L;
@@ -251,29 +277,42 @@ __device__ __forceinline__ void hc_pw_units(const T* src, int ss, int NPX, const
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const int l32 = lane & 31, h = lane >> 5;
     const int na = (M + 31) >> 5, nb = (NPX + 31) >> 5;
+    // each wave takes a contiguous range of the units in A-tile-major order, so a wave with one
+    // K piece (NH == 1) loads an A tile's fragments once for all its B tiles; the first unit's
+    // A fragments are issued before the barrier (they do not depend on the previous phase)
+    const int nu = na * nb;
+    const int u0 = (wv * nu) / NWV, u1 = ((wv + 1) * nu) / NWV;
+    const HcDiv dnb = hc_div(nb, 16);
+    uint4 af[NH > 1 ? 2 : 1][KP], bf[NH > 1 ? 2 : 1][KP];
+    auto load_a = [&](int a, int hh, int buf) {
+        const T* wrow = w + (long long)(a * 32 + l32) * wld + 8 * h + hh * KP * 16;
+#pragma unroll
+        for (int kb = 0; kb < KP; ++kb) af[buf][kb] = *reinterpret_cast<const uint4*>(wrow + kb * 16);
+    };
+    auto load_b = [&](const T* brow, int hh, int buf) {
+#pragma unroll
+        for (int kb = 0; kb < KP; ++kb) bf[buf][kb] = *reinterpret_cast<const uint4*>(brow + (hh * KP + kb) * 16);
+    };
+    int a_cur = u0 < u1 ? hc_q(u0, dnb) : 0;
+    if (u0 < u1) load_a(a_cur, 0, 0);
     hc_barrier();   // src complete
-    const HcDiv dna = hc_div(na, 16);
-    for (int u = wv; u < na * nb; u += NWV) {
-        const int bi = hc_q(u, dna), a = u - bi * na;
+    for (int u = u0; u < u1; ++u) {
+        const int a = hc_q(u, dnb), bi = u - a * nb;
         const int px = bi * 32 + l32;
         const int pxc = px < NPX ? px : NPX - 1;
         const T* brow = src + pxc * ss + 8 * h;
-        const T* wrow = w + (long long)(a * 32 + l32) * wld + 8 * h;
-        uint4 af[NH > 1 ? 2 : 1][KP], bf[NH > 1 ? 2 : 1][KP];
-        auto load = [&](int hh, int buf) {
-#pragma unroll
-            for (int kb = 0; kb < KP; ++kb) {
-                af[buf][kb] = *reinterpret_cast<const uint4*>(wrow + (hh * KP + kb) * 16);
-                bf[buf][kb] = *reinterpret_cast<const uint4*>(brow + (hh * KP + kb) * 16);
-            }
-        };
-        load(0, 0);
+        if (NH > 1 ? u > u0 : a != a_cur) load_a(a, 0, 0);
+        a_cur = a;
+        load_b(brow, 0, 0);
         f32x16 acc;
 #pragma unroll
         for (int e = 0; e < 16; ++e) acc[e] = 0.f;
 #pragma unroll
         for (int hh = 0; hh < NH; ++hh) {
-            if (hh + 1 < NH) load(hh + 1, (hh + 1) & 1);
+            if (hh + 1 < NH) {
+                load_a(a, hh + 1, (hh + 1) & 1);
+                load_b(brow, hh + 1, (hh + 1) & 1);
+            }
 #pragma unroll
             for (int kb = 0; kb < KP; ++kb) acc = HMfma<T>::step(af[hh & 1][kb], bf[hh & 1][kb], acc);
         }
@@ -339,6 +378,15 @@ __device__ __forceinline__ void hc_body(const HeadClsArgs& A, int li, char* hsm)
             hc_glds(src, lds0 + (unsigned)L.prm + (unsigned)i0 * 16);
         }
     }
+#ifdef YH_HC_TRACE
+    if (threadIdx.x == 0 && blockIdx.x < HC_TR_WG) {
+        const unsigned long long hw = (unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 4);
+        const unsigned long long xcc = (unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 20);
+        hc_trace_buf[(size_t)blockIdx.x * HC_TR + 9] = hw | (xcc << 32) | ((unsigned long long)li << 40);
+        hc_trace_buf[(size_t)blockIdx.x * HC_TR + 0] = __builtin_amdgcn_s_memrealtime();
+        hc_trace_buf[(size_t)blockIdx.x * HC_TR + 1] = __builtin_amdgcn_s_memtime();
+    }
+#endif
     const T* x = reinterpret_cast<const T*>(V.x);
     // 8-wave workgroups run every pointwise phase as (B tile, A tile) units with no
     // fragments held across phases (HC_UNITS); 4-wave ones preload them a phase ahead
@@ -347,30 +395,37 @@ __device__ __forceinline__ void hc_body(const HeadClsArgs& A, int li, char* hsm)
     if constexpr (P1 > 0) hc_pw_pre<T, NK1, P1>(reinterpret_cast<const T*>(V.pw1w), V.pw1ld, c3, A1);
 
     // 1-2. per 64-channel chunk: input tile with a 2-pixel halo (zeros outside the image =
-    //      dw1's zero padding) -> R1, then dw1 of the chunk over the MH x MW mid region -> R2
+    //      dw1's zero padding) -> R1 / X2 (alternating), then dw1 of the chunk over the MH x MW
+    //      mid region -> R2; the next chunk's DMA is issued once this one has landed, before its
+    //      depthwise conv
     const int ck = C0 < HC_CK ? C0 : HC_CK;
-    for (int cl = 0; cl < C0; cl += ck) {
-        // the padded tile (SX = ck + 8: cpp data chunks + 1 pad chunk per pixel) by LDS-DMA,
-        // zeros outside the image = dw1's zero padding
-        constexpr int cpp = (NK1 * 16 < HC_CK ? NK1 * 16 : HC_CK) >> 3, cpx = cpp + 1;
-        const int total = XH * XW * cpx;
-        {
-            const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
-            const HcDiv dxw = hc_div(XW, 16);
-            for (int i0 = wv * 64; i0 < total; i0 += HEAD_CLS_THREADS) {
-                const int q = i0 + lane;
-                const int px = q / cpx, c = q - px * cpx;
-                const int r = hc_q(px, dxw), cc = px - r * XW;
-                const int gh = h0 - 2 + r, gw = w0 - 2 + cc;
-                const bool ok = q < total && c < cpp && (unsigned)gh < (unsigned)H && (unsigned)gw < (unsigned)W;
-                const void* src = ok ? (const void*)(x + (((long long)n * H + gh) * W + gw) * V.ldx + cl + c * 8) : A.zero;
-                hc_glds(src, lds0 + (unsigned)i0 * 16);
-            }
+    // the padded tile (SX = ck + 8: cpp data chunks + 1 pad chunk per pixel) by LDS-DMA
+    constexpr int cpp = (NK1 * 16 < HC_CK ? NK1 * 16 : HC_CK) >> 3, cpx = cpp + 1;
+    const int xtotal = XH * XW * cpx;
+    auto issue_x = [&](int cl, unsigned base) {
+        const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+        const HcDiv dxw = hc_div(XW, 16);
+        for (int i0 = wv * 64; i0 < xtotal; i0 += HEAD_CLS_THREADS) {
+            const int q = i0 + lane;
+            const int px = q / cpx, c = q - px * cpx;
+            const int r = hc_q(px, dxw), cc = px - r * XW;
+            const int gh = h0 - 2 + r, gw = w0 - 2 + cc;
+            const bool ok = q < xtotal && c < cpp && (unsigned)gh < (unsigned)H && (unsigned)gw < (unsigned)W;
+            const void* src = ok ? (const void*)(x + (((long long)n * H + gh) * W + gw) * V.ldx + cl + c * 8) : A.zero;
+            hc_glds(src, lds0 + base + (unsigned)i0 * 16);
         }
+    };
+    issue_x(0, 0);
+    for (int cl = 0, k = 0; cl < C0; cl += ck, ++k) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's DMAs (and earlier loads) landed
-        hc_dw<T>(R1, XW, L.SX, R2, MH, MW, L.SD, cl, ck, PW1, C0, PB1);
-        if (cl + ck < C0) hc_barrier();   // the next chunk overwrites R1
+        if (cl == 0) HC_STAMP(2, false);
+        const unsigned cur = (k & 1) ? (unsigned)L.x2 : 0u;
+        // the other buffer's last reader (chunk k - 1's depthwise conv) ended at the barrier below
+        if (cl + ck < C0) issue_x(cl + ck, (k & 1) ? 0u : (unsigned)L.x2);
+        hc_dw<T>(reinterpret_cast<const T*>(hsm + cur), XW, L.SX, R2, MH, MW, L.SD, cl, ck, PW1, C0, PB1);
+        if (cl + ck < C0) hc_barrier();   // chunk k's buffer is re-filled with chunk k + 2
     }
+    HC_STAMP(3, false);
     // 3. pw1: D1 (R2) -> P1 (R1), zero outside the image (dw2's zero padding)
     const HcDiv dmw = hc_div(MW, 16), dtw = hc_div(TW, 16);
     auto p1_store = [&](int px, int co, uint2 v) {
@@ -387,8 +442,10 @@ __device__ __forceinline__ void hc_body(const HeadClsArgs& A, int li, char* hsm)
     constexpr int P2 = HC_UNITS ? 0 : HC_NA;
     HcA<NK2, P2> A2;   // pw2's weights, in flight during dw2
     if constexpr (P2 > 0) hc_pw_pre<T, NK2, P2>(reinterpret_cast<const T*>(V.pw2w), V.pw2ld, c3, A2);
+    HC_STAMP(4, false);
     // 4. dw2 (opens with the barrier after pw1): P1 (R1) -> D2 (R2) over the TH x TW tile
     hc_dw<T>(R1, MW, L.SM, R2, TH, TW, L.SM, 0, c3, PW2, c3, PB2);
+    HC_STAMP(5, false);
     // 5. pw2: D2 (R2) -> P2 (R1)
     auto p2_store = [&](int px, int co, uint2 v) { *reinterpret_cast<uint2*>(R1 + px * L.SM + co) = v; };
     if constexpr (P2 > 0)
@@ -396,6 +453,7 @@ __device__ __forceinline__ void hc_body(const HeadClsArgs& A, int li, char* hsm)
                               p2_store);
     else
         hc_pw_units<T, NK2>(R2, L.SM, TH * TW, reinterpret_cast<const T*>(V.pw2w), V.pw2ld, QB2, c3, true, p2_store);
+    HC_STAMP(6, false);
     HcA<NK2, P2> A3;   // pw3's weights: issued once pw2's are dead
     if constexpr (P2 > 0) hc_pw_pre<T, NK2, P2>(reinterpret_cast<const T*>(V.pw3w), V.pw3ld, A.nc, A3);
     // 6. pw3: P2 (R1) -> class logits in the head tensor, or (direct mode) their sigmoid in
@@ -427,6 +485,8 @@ __device__ __forceinline__ void hc_body(const HeadClsArgs& A, int li, char* hsm)
             if ((unsigned)gh < (unsigned)H && (unsigned)gw < (unsigned)W)
                 *reinterpret_cast<uint2*>(y + (((long long)n * H + gh) * W + gw) * V.ldy + co) = v;
         });
+    HC_STAMP(7, false);
+    HC_STAMP(8, true);
 }
 
 #if YH_HEAD_CLS_THREADS >= 512
@@ -583,7 +643,7 @@ static bool hc_div_exact(int TH, int TW, int C0, int c3, int nc) {
         if (DW * per_g >= (1 << 16) || ng * per_g * per_g >= (1 << 24)) return false;
     }
     const long long na = (std::max(c3, nc) + 31) / 32, nb = (MH * MW + 31) / 32;
-    return na * nb * na < (1 << 16);
+    return na * nb * nb < (1 << 16);   // hc_pw_units: unit index / nb
 }
 
 int head_cls_lds(int TH, int TW, int C0, int c3, int nc) {
@@ -616,6 +676,13 @@ static int launch_head_cls_t(const HeadClsArgs& a, hipStream_t s) {
     hipLaunchKernelGGL((head_cls<T>), dim3((unsigned)grid), dim3(HEAD_CLS_THREADS), lds, s, a);
     return (int)hipGetLastError();
 }
+
+#ifdef YH_HC_TRACE
+extern "C" int yh_debug_hc_trace(unsigned long long* dst, int n) {
+    if (n > HC_TR_WG * HC_TR) n = HC_TR_WG * HC_TR;
+    return (int)hipMemcpyFromSymbol(dst, HIP_SYMBOL(hc_trace_buf), (size_t)n * 8, 0, hipMemcpyDeviceToHost);
+}
+#endif
 
 int launch_head_cls(int dtype, const HeadClsArgs& a, hipStream_t s) {
     switch (dtype) {
