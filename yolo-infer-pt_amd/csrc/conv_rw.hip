@@ -41,6 +41,7 @@ namespace yh {
 
 typedef __attribute__((ext_vector_type(16))) float rw_f32x16;
 typedef __attribute__((ext_vector_type(4))) unsigned int rw_u32x4;
+typedef __attribute__((ext_vector_type(2))) unsigned int rw_u32x2;
 typedef __attribute__((ext_vector_type(2))) float rw_f32x2;
 
 RwGeo rw_geo(int S, int cin, int ncg, int npg, int mb, int tw, bool res, int nkc) {
@@ -55,15 +56,16 @@ RwGeo rw_geo(int S, int cin, int ncg, int npg, int mb, int tw, bool res, int nkc
     g.nbi = (g.pr * g.pc * g.cpp + 64 * g.nw - 1) / (64 * g.nw);
     g.nbr = res ? (g.tpx * ncg * 4 + 64 * g.nw - 1) / (64 * g.nw) : 0;
     g.slot = (g.nbi + g.nbr) * g.nw * 1024;
-    g.red = (nkc - 1) * ncg * npg * mb * 4096;
-    // coalesced epilogue: one 32-pixel x 32-cout staging tile per storing wave, + the slice's bias,
-    // + the counter mode's slot counters (2 x 8 words)
-    g.epi = ncg * npg * 2048 + ncg * 128 + 64;
+    // K-split layers: every chunk's fp32 partial tile in LDS (the reduction and the epilogue
+    // are shared by the chunk waves); otherwise one 32-pixel x 32-cout staging tile per wave for
+    // the coalesced epilogue. + the slice's bias, + the counter mode's slot counters (2 x 8 words)
+    g.red = nkc > 1 ? nkc * ncg * npg * mb * 4096 : 0;
+    g.epi = (nkc > 1 ? 0 : ncg * npg * 2048) + ncg * 128 + 64;
     return g;
 }
 
 // ablation switches of the micro benchmark (tools/micro, -DYH_ABLATION); off in the shipped
-// library: dbg 4 no MFMA, 8 no epilogue; trace = per-workgroup stamps (entry, prologue done,
+// library: dbg 4 no MFMA, 8 no epilogue stores, 16 no K-chunk reduction and no epilogue; trace = per-workgroup stamps (entry, prologue done,
 // first tile done, exit)
 #ifdef YH_ABLATION
 #define RW_DBG(bit) (p.dbg & (bit))
@@ -170,13 +172,15 @@ __global__ __launch_bounds__(64 * NCG * NKC * NPG, (NCG * NKC * NPG >= 8 || NCG 
     constexpr int RSH = NCG == 1 ? 2 : NCG == 2 ? 1 : 0;   // residual image swizzle: chunk ^ (px >> RSH)
     constexpr int NBR = RES ? (TPX * RCH + 64 * NW - 1) / (64 * NW) : 0;
     constexpr int SLOT = (NBI + NBR) * NW * 1024;
-    constexpr int RED = (NKC - 1) * NCG * NPG * MB * 4096;   // K-chunk partials (rw_geo's red)
+    constexpr int RED = NKC > 1 ? NKC * NCG * NPG * MB * 4096 : 0;   // K-chunk partials (rw_geo's red)
+    constexpr int EST = NKC > 1 ? 0 : NCG * NPG * 2048;              // epilogue staging tiles (NKC = 1)
     static_assert(TPX % TW == 0 && (CPP & (CPP - 1)) == 0 && NS >= 2 && NKT % NKC == 0, "rw geometry");
     // VMEM ops a wave issues after its DMAs of tile it, still uncounted at the wait of
-    // iteration it: the epilogues (2 stores per B tile; only the chunk-0 waves store) of the
-    // NS-1 earlier tiles and the DMAs of NS-2 tiles
-    constexpr int CNT0 = (NS - 1) * 2 * MB + (NS - 2) * (NBI + NBR);
-    constexpr int CNT1 = (NS - 2) * (NBI + NBR);
+    // iteration it: the epilogues of the NS-1 earlier tiles (NKC = 1: 2 stores per B tile;
+    // K-split: 4 / NKC per B tile from every chunk wave) and the DMAs of NS-2 tiles
+    constexpr int SPT = NKC > 1 ? MB * (4 / NKC) : 2 * MB;
+    constexpr int CNT0 = (NS - 1) * SPT + (NS - 2) * (NBI + NBR);
+    static_assert(NKC == 1 || NKC == 2 || NKC == 4, "K chunks");
     static_assert(CNT0 <= 63, "vmcnt range");
     // counter mode: tiles issued D = NS - 2 ahead; at the wait for tile it's DMA, the wave has
     // issued since then the DMAs of D - 1 tiles and the stores of D epilogues
@@ -324,14 +328,14 @@ __global__ __launch_bounds__(64 * NCG * NKC * NPG, (NCG * NKC * NPG >= 8 || NCG 
     }
     // the slice's bias in LDS (read per B tile in the epilogue: 16 VGPRs free for the fragment
     // prefetch ring)
-    float* bias_l = reinterpret_cast<float*>(reinterpret_cast<char*>(sm4) + NS * SLOT + RED + NCG * NPG * 2048);
+    float* bias_l = reinterpret_cast<float*>(reinterpret_cast<char*>(sm4) + NS * SLOT + RED + EST);
     if ((int)threadIdx.x < NCG * 32) bias_l[threadIdx.x] = p.bias[(sl * NCG) * 32 + threadIdx.x];
     // the compiler waits for these loads HERE (not at their first use inside the loop,
     // where its vmcnt(0) would drain the patch ring every iteration)
 #pragma unroll
     for (int s = 0; s < NKS; ++s) asm volatile("" :: "v"(wf[s].x), "v"(wf[s].y), "v"(wf[s].z), "v"(wf[s].w));
     // counter mode: landed[NS] then done[NS], zeroed before the barrier below
-    unsigned* cnt = reinterpret_cast<unsigned*>(reinterpret_cast<char*>(sm4) + NS * SLOT + RED + NCG * NPG * 2048 + NCG * 128);
+    unsigned* cnt = reinterpret_cast<unsigned*>(reinterpret_cast<char*>(sm4) + NS * SLOT + RED + EST + NCG * 128);
     if (CM && (int)threadIdx.x < 2 * NS) cnt[threadIdx.x] = 0u;
     rw_vmwait<0>();
     rw_barrier();
@@ -399,6 +403,71 @@ __global__ __launch_bounds__(64 * NCG * NKC * NPG, (NCG * NKC * NPG >= 8 || NCG 
             }
         }
     };
+    // ---- K-split epilogue: the NKC chunk waves of a (cg, pg) tile share the reduction and the
+    //      epilogue. Every chunk's fp32 partials sit in LDS ([chunk][pg][cg][j] tiles: 32 pixel
+    //      rows of 8 16-B chunks of 4 couts, chunk c of pixel p at c ^ (p & 7)); wave kc takes
+    //      pixels kc * 32 / NKC .. of each B tile, lane (pixel, 4-cout chunk c4) sums its four
+    //      couts in chunk order (((P0 + P1) + P2) + P3: the canonical order), adds the bias,
+    //      activates, rounds (+ residual, rounded again) and stores 8 B; 8 lanes write a
+    //      pixel's 64 contiguous bytes.
+    auto red_tile = [&](int k2, int j) {
+        return reinterpret_cast<float*>(reinterpret_cast<char*>(sm4) + NS * SLOT) +
+               (((k2 * NPG + pg) * NCG + cg) * MB + j) * 1024;
+    };
+    auto epilogue_split = [&](int it) {
+        int n, ty0, tx0;
+        tile_pos(it, n, ty0, tx0);
+        constexpr int PPW = 32 / NKC, NR = PPW / 8;
+        const int c4 = lane & 7;
+        const float4 bv = *reinterpret_cast<const float4*>(bias_l + cg * 32 + 4 * c4);
+#pragma unroll
+        for (int j = 0; j < MB; ++j) {
+#pragma unroll
+            for (int r = 0; r < NR; ++r) {
+                const int pp = kc * PPW + r * 8 + (lane >> 3);
+                const int off = pp * 32 + (c4 ^ (pp & 7)) * 4;
+                float4 v = *reinterpret_cast<const float4*>(red_tile(0, j) + off);
+#pragma unroll
+                for (int k2 = 1; k2 < NKC; ++k2) {
+                    const float4 u = *reinterpret_cast<const float4*>(red_tile(k2, j) + off);
+                    v.x += u.x; v.y += u.y; v.z += u.z; v.w += u.w;
+                }
+                float x0 = v.x + bv.x, x1 = v.y + bv.y, x2 = v.z + bv.z, x3 = v.w + bv.w;
+                // selects, not a branch: one basic block the scheduler can spread between MFMAs
+                x0 = silu_act ? silu<T>(x0) : x0;
+                x1 = silu_act ? silu<T>(x1) : x1;
+                x2 = silu_act ? silu<T>(x2) : x2;
+                x3 = silu_act ? silu<T>(x3) : x3;
+                unsigned w[2] = {rw_pack2<T>(x0, x1), rw_pack2<T>(x2, x3)};
+                const int px = (pg * MB + j) * 32 + pp;
+                const int oy = ty0 + px / TW, ox = tx0 + px % TW;
+                const bool ok = oy < p.Ho && ox < p.Wo;
+                const long long m = ((long long)n * p.Ho + oy) * p.Wo + ox;
+                if constexpr (RES) {
+                    const int f = (px >> RSH) & (RCH - 1);
+                    const char* rb = reinterpret_cast<const char*>(sm4) + (it % NS) * SLOT + NBI * NW * 1024 + px * RCH * 16;
+                    const uint2 rr = *reinterpret_cast<const uint2*>(rb + ((cg * 4 + (c4 >> 1)) ^ f) * 16 + (c4 & 1) * 8);
+                    const unsigned rv[2] = {rr.x, rr.y};
+#pragma unroll
+                    for (int q = 0; q < 2; ++q)
+                        w[q] = rw_pack2<T>(rw_lo<T>(w[q]) + rw_lo<T>(rv[q]), rw_hi<T>(w[q]) + rw_hi<T>(rv[q]));
+                }
+                const unsigned oo = ok ? (unsigned)(m * p.ldo * 2) + (unsigned)(co0 + 4 * c4) * 2u : RW_OOB;
+                const unsigned od = RW_DBG(8) ? RW_OOB : oo;
+                __builtin_amdgcn_raw_buffer_store_b64(rw_u32x2{w[0], w[1]}, ro, od, 0, 0);
+            }
+        }
+    };
+    // K-split layers without a residual run tile it - 1's epilogue in iteration it, beside tile
+    // it's MFMAs (the partials wait in LDS; the residual would sit in a slot the ring has already
+    // re-filled). Iteration 0 issues the same number of stores to the dropped offset, so the
+    // vmcnt arithmetic (CNT0) holds from the first iteration on.
+    constexpr bool DEFER = NKC > 1 && !RES && !CM;
+    auto dummy_stores = [&]() {
+        constexpr int NR = 32 / NKC / 8;
+#pragma unroll
+        for (int k = 0; k < MB * NR; ++k) __builtin_amdgcn_raw_buffer_store_b64(rw_u32x2{0u, 0u}, ro, RW_OOB, 0, 0);
+    };
     unsigned long long t_wait = 0ull;   // diagnostic builds, dbg 64: time spent in the loop-top waits
     if constexpr (CM) {
         // the prologue issued tiles 0 .. NS - 2; tiles 0 .. DPC - 1 are the ones this loop expects
@@ -427,13 +496,16 @@ __global__ __launch_bounds__(64 * NCG * NKC * NPG, (NCG * NKC * NPG >= 8 || NCG 
             }
         } else if (it > 0) {
             const unsigned long long tw0 = (RW_TRACE && RW_DBG(64)) ? __builtin_amdgcn_s_memrealtime() : 0ull;
-            if (kc == 0) rw_vmwait<CNT0>();
-            else rw_vmwait<CNT1>();
+            rw_vmwait<CNT0>();
             rw_barrier();   // tile it complete in its slot; slot (it - 1) % NS read by every wave
             if (RW_TRACE && RW_DBG(64)) t_wait += __builtin_amdgcn_s_memrealtime() - tw0;
             if (RW_TRACE && it == 1) t_first = __builtin_amdgcn_s_memrealtime();
         }
         if constexpr (!CM) issue(it + NS - 1, (it + NS - 1) % NS);
+        if constexpr (DEFER) {
+            if (it > 0) epilogue_split(it - 1);
+            else dummy_stores();
+        }
 
         // ---- MFMAs: one k-step = one 32x32x16 step per B tile, fragments of step s+1
         //      read while step s multiplies
@@ -467,31 +539,31 @@ __global__ __launch_bounds__(64 * NCG * NKC * NPG, (NCG * NKC * NPG >= 8 || NCG 
             }
         }
 
-        // ---- K chunks: the partials of chunks 1.. through LDS ([chunk][pg][cg][j][reg][lane]
-        //      floats, lane-consecutive), added by the chunk-0 wave in chunk order
+        if (RW_DBG(16)) continue;   // ablation: no K-chunk reduction, no epilogue
+        // ---- K chunks: every chunk wave's partial tile to LDS (lane (r32, h) holds couts
+        //      16 h .. 16 h + 15 of pixel r32: 4 swizzled 16-B chunks), then the shared epilogue
         if constexpr (NKC > 1) {
-            float* red = reinterpret_cast<float*>(reinterpret_cast<char*>(sm4) + NS * SLOT);
-            auto rslot = [&](int k2, int j) { return red + ((((k2 - 1) * NPG + pg) * NCG + cg) * MB + j) * 1024 + lane; };
-            if (kc > 0) {
+            if constexpr (DEFER) rw_barrier();   // every wave's epilogue reads of tile it - 1 are done
 #pragma unroll
-                for (int j = 0; j < MB; ++j)
+            for (int j = 0; j < MB; ++j) {
+                float* t = red_tile(kc, j) + r32 * 32;
 #pragma unroll
-                    for (int e = 0; e < 16; ++e) rslot(kc, j)[e * 64] = acc[j][e];
+                for (int q = 0; q < 4; ++q)
+                    *reinterpret_cast<float4*>(t + (((4 * h + q) ^ (r32 & 7)) * 4)) =
+                        make_float4(acc[j][4 * q], acc[j][4 * q + 1], acc[j][4 * q + 2], acc[j][4 * q + 3]);
             }
-            rw_barrier();
-            if (kc == 0) {
-#pragma unroll
-                for (int k2 = 1; k2 < NKC; ++k2) {
-#pragma unroll
-                    for (int j = 0; j < MB; ++j)
-#pragma unroll
-                        for (int e = 0; e < 16; ++e) acc[j][e] += rslot(k2, j)[e * 64];
-                    asm volatile("" ::: "memory");   // one chunk's 16 x MB reads in flight, not all
-                }
+            if constexpr (!DEFER) {
+                rw_barrier();
+                epilogue_split(it);
             }
+        } else {
+            epilogue(it);
         }
-        if (kc == 0) epilogue(it);
         if constexpr (CM) rw_signal(cnt + NS + it % NS, lane);
+    }
+    if constexpr (DEFER) {
+        rw_barrier();   // the last tile's partials
+        epilogue_split(n_it - 1);
     }
     if (RW_TRACE && threadIdx.x == 0) {
         unsigned long long* tr = RW_TRACE + blockIdx.x * 4;
