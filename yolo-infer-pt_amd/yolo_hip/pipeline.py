@@ -62,8 +62,14 @@ class DetectPipeline:
         # nms_on_lane: each batch's NMS follows its forward on the lane's stream (one
         # stream fewer: the HIP runtime maps streams onto GPU_MAX_HW_QUEUES = 4 queues)
         self.nms_stream = None if nms_on_lane else torch.cuda.Stream(device=dev)
-        # lane 0 runs on the caller's stream, the others on streams of their own
-        self.lane_streams = [None] + [torch.cuda.Stream(device=dev) for _ in self.engs[1:]]
+        # every lane on a stream of its own: the caller's stream then holds only the caller's
+        # work, so the event a lane waits on before reading x (recorded there at submit) does
+        # not also wait for an earlier forward (with lane 0 on the caller's stream every other
+        # lane's forward k waited for lane 0's forward k - 1). YH_LANE0_MAIN=1: the old layout.
+        import os
+        lane0_main = os.environ.get("YH_LANE0_MAIN", "0") == "1" or len(self.engs) == 1
+        self.lane_streams = ([None] if lane0_main else [torch.cuda.Stream(device=dev)]) + \
+            [torch.cuda.Stream(device=dev) for _ in self.engs[1:]]
         self.post = post
         self.nms_kwargs = nms_kwargs or {}
         self.k = 0
@@ -110,8 +116,8 @@ class DetectPipeline:
     def drain(self):
         """Make the caller's stream wait for every NMS in flight."""
         main = torch.cuda.current_stream(self.eng.device)
-        if len(self.engs) > 1:   # forwards still running on the lane streams
-            for fs in self.lane_streams[1:]:
+        for fs in self.lane_streams:   # forwards still running on the lane streams
+            if fs is not None:
                 main.wait_stream(fs)
         for e in self.free:
             if e is not None:
