@@ -11,7 +11,7 @@ OBJDIR ?= build/obj
 HIPFLAGS := --offload-arch=$(ARCH) -O3 -fPIC -std=c++17 -Iinclude -I$(SRC) \
             -fhip-fp32-correctly-rounded-divide-sqrt -Wno-unused-result $(EXTRA)
 OBJS := $(OBJDIR)/engine.o $(OBJDIR)/conv.o $(OBJDIR)/misc.o $(OBJDIR)/nms.o $(OBJDIR)/conv_mx.o $(OBJDIR)/nms_host.o \
-        $(OBJDIR)/preprocess.o $(OBJDIR)/head.o $(OBJDIR)/c3k2.o $(OBJDIR)/conv_rw.o $(OBJDIR)/c3k.o $(OBJDIR)/boxc.o
+        $(OBJDIR)/preprocess.o $(OBJDIR)/head.o $(OBJDIR)/c3k2.o $(OBJDIR)/conv_rw.o $(OBJDIR)/c3k.o $(OBJDIR)/boxc.o $(OBJDIR)/pwchain.o
 
 all: $(OUT)
 
@@ -46,6 +46,9 @@ $(OBJDIR)/c3k.o: $(SRC)/c3k.hip $(SRC)/common.h $(SRC)/dtypes.h | $(OBJDIR)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
 $(OBJDIR)/boxc.o: $(SRC)/boxc.hip $(SRC)/common.h $(SRC)/dtypes.h | $(OBJDIR)
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+$(OBJDIR)/pwchain.o: $(SRC)/pwchain.hip $(SRC)/common.h $(SRC)/dtypes.h | $(OBJDIR)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
 $(OBJDIR)/preprocess.o: $(SRC)/preprocess.hip $(SRC)/common.h include/yolo_hip.h | $(OBJDIR)

@@ -113,8 +113,10 @@ def test_c3k_block_equals_per_layer_launches(gpu, variant, dtype, batch, h, w, n
     c = 256). YH_C3K=0 keeps the seven per-layer launches everywhere. Bit-identical either way."""
     model = make_model(variant)
     x = synth.synth_scenes(batch, h, w, seed=37).to(gpu, dtype)
-    fused = _engine(model, dtype, gpu, True)
-    plain = _engine(model, dtype, gpu, True, YH_C3K="0")
+    # pointwise chains off in both: with YH_C3K=0 the per-layer C3k 1x1 convs would form chains
+    # of their own and change the launch count this test compares
+    fused = _engine(model, dtype, gpu, True, YH_PWCHAIN="0")
+    plain = _engine(model, dtype, gpu, True, YH_C3K="0", YH_PWCHAIN="0")
     yf = fused.forward(x).clone()
     yp = plain.forward(x).clone()
     kinds_f = [u["cls"] for u in fused.units(batch, h, w)]
@@ -283,5 +285,36 @@ def test_box_chain_equals_per_layer_launches(gpu, variant, dtype, batch, h, w):
     assert "head.box" in lf and "head.box_dfl" not in lf and not any(l.startswith("head.box.") for l in lf), lf
     assert "head.box" not in lp and "head.box_dfl" in lp
     assert len(lp) - len(lf) == 6
+    assert torch.isfinite(yf.float()).all()
+    assert torch.equal(yf, yp), (yf.float() - yp.float()).abs().max().item()
+
+
+@pytest.mark.parametrize("variant,dtype,batch,h,w,nchain", [("n", torch.bfloat16, 2, 640, 640, 3),
+                                                           ("n", torch.float16, 3, 96, 160, 3),
+                                                           ("n", torch.bfloat16, 32, 640, 640, 3),
+                                                           ("s", torch.float16, 2, 640, 640, 3),
+                                                           ("x", torch.bfloat16, 1, 640, 640, 3),
+                                                           ("n", torch.bfloat16, 1, 1280, 1280, 3)])
+def test_pw_chain_equals_per_layer_launches(gpu, variant, dtype, batch, h, w, nchain):
+    """pwchain.hip: runs of consecutive 1x1 convs on a 40x40-or-smaller map (the C3k2 conv2 ->
+    SPPF conv1 pair, SPPF conv2 -> C2PSA conv1 -> qkv, and the PSABlock after the attention core:
+    proj (+x) -> ffn -> ffn (+x) -> C2PSA conv2 over [a | b]) as one launch each, the stage
+    outputs a later stage reads kept in LDS, are bit-identical to the per-layer launches
+    (YH_PWCHAIN=0): 64- and 32-pixel workgroups (s, x: the wider stages take 32), a partial last
+    workgroup (96x160: a 3x5 map at the coarsest level), concat inputs split between LDS and global
+    sources, residuals from LDS and from global."""
+    model = make_model(variant)
+    x = synth.synth_scenes(batch, h, w, seed=47).to(gpu, dtype)
+    fused = _engine(model, dtype, gpu, True)
+    plain = _engine(model, dtype, gpu, True, YH_PWCHAIN="0")
+    yf = fused.forward(x).clone()
+    yp = plain.forward(x).clone()
+    uf = fused.units(batch, h, w)
+    up = plain.units(batch, h, w)
+    chains = [u["label"] for u in uf if u["cls"] == "pw_chain"]
+    print(variant, h, w, chains)
+    assert len(chains) >= nchain, [u["label"] for u in uf]   # s / x: more runs at 40x40 too
+    assert "pw_chain" not in [u["cls"] for u in up]
+    assert len(up) > len(uf)
     assert torch.isfinite(yf.float()).all()
     assert torch.equal(yf, yp), (yf.float() - yp.float()).abs().max().item()

@@ -126,6 +126,36 @@ def _check_op(d, ins, outs, x, y, H, W, nc, params, dtype):
                 lo, hi = oc.layer(lo, hi, c1, params, dtype)
                 return oc.dfl_box(*oc.layer(lo, hi, c2, params, dtype), 8 << l, dtype)
             cases.append((f"level {l} boxes", y[:, 0:4, a0:a0 + h * w], fn))
+    elif kind == "pw_chain":
+        # stage by stage: inputs from the device operands (captured before the chain ran) or from
+        # an earlier stage's output interval; compared where no later stage overwrote the output
+        def chain_iv():
+            iv = []
+            for k, stg in enumerate(d["stages"]):
+                conv = d["convs"][k]
+                los, his = [], []
+                for r in stg["runs"]:
+                    if r["src"] < 0:
+                        t = ins[f"s{k}.in{r['seg']}"][:, r["off"]:r["off"] + r["n"]]
+                        los.append(t)
+                        his.append(t)
+                    else:
+                        lo, hi = iv[r["src"]]
+                        los.append(lo[:, r["soff"]:r["soff"] + r["n"]])
+                        his.append(hi[:, r["soff"]:r["soff"] + r["n"]])
+                res = None
+                if stg["res"] == -1:
+                    res = oc.exact(ins[f"s{k}.res"][:, :conv["cout"]])
+                elif stg["res"] >= 0:
+                    lo, hi = iv[stg["res"]]
+                    o = stg["res_off"]
+                    res = (lo[:, o:o + conv["cout"]], hi[:, o:o + conv["cout"]])
+                iv.append(oc.layer(torch.cat(los, 1), torch.cat(his, 1), conv, params, dtype, res=res))
+            return iv
+        for k, stg in enumerate(d["stages"]):
+            if stg["final"]:
+                cases.append((f"stage {k} out", _nchw(outs[f"s{k}.out"])[:, :d["convs"][k]["cout"]],
+                              lambda k=k: chain_iv()[k]))
     elif kind == "decode":
         for l in range(3):
             L = ins[f"L{l}"]
@@ -172,12 +202,12 @@ def run_op_parity(gpu, variant, dtype, batch, size, images, seed):
             continue
         ins = {}
         for s, o in enumerate(d["operands"]):
-            if o["role"] in IN_ROLES:
+            if o["role"] in IN_ROLES or o["role"].split(".")[-1] in IN_ROLES:
                 ins[o["role"]] = _nchw(eng.debug_operand(i, s, batch, d)[img].cpu()).double()
         eng.debug_run(x, yd, i, i + 1)
         outs = {}
         for s, o in enumerate(d["operands"]):
-            if o["role"] not in IN_ROLES:
+            if not (o["role"] in IN_ROLES or o["role"].split(".")[-1] in IN_ROLES):
                 outs[o["role"]] = eng.debug_operand(i, s, batch, d)[img].cpu()
         torch.cuda.synchronize()
         st = _check_op(d, ins, outs, x_sel, yd[img].cpu(), H, W, nc, params, dtype)
@@ -193,7 +223,7 @@ def run_op_parity(gpu, variant, dtype, batch, size, images, seed):
             # chains, where a layer's undecided roundings (1 ulp either way, both legitimate) feed
             # the next layer's K-sum, nor for attention, whose softmax weights are rounded to the
             # dtype for the P.V MFMA (r05: 2-6 % of its outputs; the interval accounts for both)
-            multi = d["kind"] in ("stem_fused", "c3k2", "c3k", "head_cls", "box_chain", "attention")
+            multi = d["kind"] in ("stem_fused", "c3k2", "c3k", "head_cls", "box_chain", "attention", "pw_chain")
             if s["bad"] or (not multi and s["over1"] > 1e-3):
                 failures.append((d["label"], kernels[i], s))
     assert not failures, failures[:4]
@@ -204,7 +234,7 @@ def run_op_parity(gpu, variant, dtype, batch, size, images, seed):
 
 def test_op_parity_c2_n_bf16_b32(gpu):
     kinds, n = run_op_parity(gpu, "n", torch.bfloat16, 32, 640, (0, 17, 31), seed=21)
-    assert {"stem_fused", "conv", "c3k2", "c3k", "sppf", "attention", "head_cls", "box_dfl"} <= kinds, kinds
+    assert {"stem_fused", "conv", "c3k2", "c3k", "sppf", "attention", "head_cls", "box_dfl", "pw_chain"} <= kinds, kinds
 
 
 def test_op_parity_n_fp16(gpu):

@@ -23,6 +23,8 @@ FAMILY = {  # dispatch-name patterns per op class (yolo_hip.engine.OP_CLASSES); 
     "box_dfl": r"box_dfl",
     "c3k2": r"csp_fused",
     "c3k": r"c3k_fused",
+    "box_chain": r"box_chain",
+    "pw_chain": r"pw_chain",
 }
 
 

@@ -260,6 +260,42 @@ bool bx_ok(int C0);
 bool bx_tile(int H, int W, int& TH, int& TW);
 int launch_box_chain(int dtype, const BoxChainArgs& a, hipStream_t s);
 
+// Pointwise chain (pwchain.hip): consecutive 1x1 convs of one map as one launch. A workgroup
+// owns P consecutive pixels (flattened n, h, w) and runs the stages in order; a stage's input
+// channels come in runs of whole 128-channel pieces, each from the LDS copy of an earlier
+// stage's output or from a global view loaded into LDS in the prologue.
+constexpr int PWC_THREADS = 512;
+constexpr int PWC_MAX_STAGES = 6, PWC_MAX_RUNS = 4, PWC_MAX_LOADS = 6;
+struct PwcRun {
+    int lds;   // LDS byte offset of the run's first channel at pixel 0
+    int ld;    // pixel stride of that LDS region (elements)
+    int nkb;   // 16-channel blocks (a multiple of 8)
+};
+struct PwcStage {
+    int K, N, act, nrun;
+    PwcRun run[PWC_MAX_RUNS];
+    const void* w; int wld;            // row-major [>= N][wld] 16-bit weights (conv's w_dev, ld Kp)
+    const float* bias;                 // >= N floats
+    int res_lds, res_ldl;              // residual in LDS (byte offset of channel 0, stride) or -1; a
+                                       // residual no stage of the chain writes comes by the prologue
+    void* out; int ldo;                // global output view (channel 0) and pixel stride
+    int out_lds, out_ldl;              // LDS copy of the output (byte offset, stride) or -1
+};
+struct PwcLoad {
+    const void* g; int ldg;            // global view (channel 0) and pixel stride (elements)
+    int lds;                           // LDS byte offset; pixel stride nchunk + 1 16-B chunks
+    int nchunk;                        // 16-B chunks (8 channels) per pixel
+};
+struct PwChainArgs {
+    long long M;                       // pixels of the map (B * H * W)
+    int P, nst, nload;
+    int sink;                          // LDS byte offset of a scratch KB (weight warm-up DMAs)
+    PwcStage st[PWC_MAX_STAGES];
+    PwcLoad ld[PWC_MAX_LOADS];
+    const void* zero;                  // >= 16 zero bytes
+};
+int launch_pw_chain(int dtype, const PwChainArgs& a, int lds, hipStream_t s);
+
 // launchers (return hipError_t as int)
 bool conv_kernel_ok(int dtype, int kern, const ConvArgs& a);
 int launch_conv(int dtype, int kern, int BM, int BN, const ConvArgs& a, hipStream_t s);

@@ -76,7 +76,7 @@ static uint16_t f2h(float f) {
 // ---------------------------------------------------------------- graph model
 enum ConvKind { CK_DENSE = 0, CK_FIRST = 1, CK_DW = 2, CK_PE = 3 };
 enum OpKind { OP_FIRST, OP_CONV, OP_DW, OP_SPPF, OP_ATTN, OP_DECODE, OP_HEADCLS, OP_BOXDFL, OP_CSP, OP_STEM2, OP_C3K,
-              OP_BOXCHAIN };
+              OP_BOXCHAIN, OP_PWCHAIN };
 static const char* op_kind_name(OpKind k) {
     switch (k) {
         case OP_FIRST: return "stem";
@@ -91,11 +91,12 @@ static const char* op_kind_name(OpKind k) {
         case OP_C3K: return "c3k";
         case OP_STEM2: return "stem_fused";
         case OP_BOXCHAIN: return "box_chain";
+        case OP_PWCHAIN: return "pw_chain";
     }
     return "unknown";
 }
 enum OpClass { CL_CONV3 = 0, CL_CONV1 = 1, CL_FIRST = 2, CL_DW = 3, CL_SPPF = 4, CL_ATTN = 5, CL_DECODE = 6,
-               CL_HEADCLS = 7, CL_BOXDFL = 8, CL_CSP = 9, CL_C3K = 10, CL_BOXCHAIN = 11, CL_N = 12 };
+               CL_HEADCLS = 7, CL_BOXDFL = 8, CL_CSP = 9, CL_C3K = 10, CL_BOXCHAIN = 11, CL_PWCHAIN = 12, CL_N = 13 };
 
 struct Tensor { int level; int C; };        // physical channels = pixel stride
 struct View { int t = -1; int coff = 0; int C = 0; };
@@ -148,6 +149,15 @@ struct Op {
     // ops it replaces at shapes where every level has a tile (bops: box.l.0 per level first)
     int bxc[3][3] = {{-1, -1, -1}, {-1, -1, -1}, {-1, -1, -1}};
     std::vector<int> alts;
+    // OP_PWCHAIN: alts = the member 1x1 conv ops (stages, in order); per stage its input runs
+    // (16-channel blocks in weight order: LDS region of an earlier stage's output, or a
+    // prologue-loaded global view), its residual and whether its output is kept in LDS
+    struct PwRun { int stage = -1; int coff = 0; int nch = 0; int load = -1; };   // coff: channel in the source
+    struct PwStage { std::vector<PwRun> runs; int res_stage = -2; int res_coff = 0; int res_load = -1; bool keep = false; int lds = -1; };
+    std::vector<PwStage> pws;
+    std::vector<View> pwl;          // prologue loads (global views)
+    std::vector<int> pwl_lds;       // their LDS byte offsets
+    int pwP = 0, pwLds = 0;
     std::string label;
 };
 
@@ -174,12 +184,13 @@ struct GraphKey {
 // YH_C3K=0 keeps the C3k blocks as per-layer launches (compared bit for bit by the tests),
 // YH_HCLS_WIDE=0 keeps a 256-channel level's cls branch (v11_n 20x20) as per-layer launches.
 struct Options {
-    bool fuse = true, csp_tail = false, tune_log = false, c3k = true, hcls_wide = true, box_chain = false;
+    bool fuse = true, csp_tail = false, tune_log = false, c3k = true, hcls_wide = true, box_chain = false, pw_chain = true;
     int conv_force = -1;
     static Options from_env() {
         Options o;
         if (const char* e = getenv("YH_FUSE")) o.fuse = atoi(e) != 0;
         if (const char* e = getenv("YH_BOXCHAIN")) o.box_chain = atoi(e) != 0;
+        if (const char* e = getenv("YH_PWCHAIN")) o.pw_chain = atoi(e) != 0;
         if (const char* e = getenv("YH_CSP_TAIL")) o.csp_tail = atoi(e) != 0;
         if (const char* e = getenv("YH_C3K")) o.c3k = atoi(e) != 0;
         if (const char* e = getenv("YH_HCLS_WIDE")) o.hcls_wide = atoi(e) != 0;
@@ -570,6 +581,157 @@ struct Net {
             ops.push_back(dec);
         }
         finalize_convs();
+        fuse_pw_chains();
+    }
+
+    // ---- pointwise chains (pwchain.hip): maximal runs of consecutive 1x1 conv ops on one
+    //      40x40-or-smaller map become one launch, inserted after the run's last op; the per-layer
+    //      ops stay (inactive) for YH_PWCHAIN=0 and the parity tests
+    void fuse_pw_chains() {
+        if (dtype == F32 || !opt.fuse || !opt.pw_chain) return;
+        for (size_t i = 0; i < ops.size();) {
+            std::vector<char> taken(ops.size(), 0);   // per-layer alternatives of another fused op
+            for (auto& o : ops) {
+                for (int k = o.alt0; k >= 0 && k < o.alt1; ++k) taken[k] = 1;
+                if (o.kind != OP_PWCHAIN)
+                    for (int k : o.alts) taken[k] = 1;
+            }
+            auto eligible = [&](size_t k) {
+                const Op& o = ops[k];
+                if (o.kind != OP_CONV || taken[k]) return false;
+                const ConvDesc& d = convs[o.conv];
+                if (d.k != 1 || d.stride != 1 || d.cout % 32 || d.K % 128 || d.K > 1024 || d.cout > 1024) return false;
+                const int lv = tensors[o.out.t].level;
+                if (lv < 4 || o.out.coff % 8) return false;
+                for (size_t si = 0; si < o.in.size(); ++si) {
+                    const Seg& sg = o.in[si];
+                    if (sg.up || tensors[sg.v.t].level != lv || d.segs[si].first != d.segs[si].second) return false;
+                }
+                if (o.has_res && (tensors[o.res.t].level != lv || o.res.C < d.cout)) return false;
+                return true;
+            };
+            if (!eligible(i)) { ++i; continue; }
+            const int lv = tensors[ops[i].out.t].level;
+            size_t j = i + 1;
+            while (j < ops.size() && j - i < (size_t)PWC_MAX_STAGES && eligible(j) && tensors[ops[j].out.t].level == lv) ++j;
+            size_t made = 0;
+            for (size_t e = j; e >= i + 2 && !made; --e)
+                if (make_pw_chain(i, e)) made = e + 1;   // the chain op sits at e
+            i = made ? made : i + 1;
+        }
+    }
+    // the chain ops [i, e) as one OP_PWCHAIN inserted at e; false (nothing changed) if the stages'
+    // sources do not split into whole 128-channel runs or the tile does not fit the LDS
+    bool make_pw_chain(size_t i, size_t e) {
+        const int n = (int)(e - i);
+        Op ch;
+        ch.kind = OP_PWCHAIN;
+        ch.pws.resize(n);
+        // the latest stage before k writing channel c of tensor t (-1: none)
+        auto producer = [&](int k, int t, int c) {
+            for (int q = k - 1; q >= 0; --q) {
+                const View& o = ops[i + q].out;
+                if (o.t == t && c >= o.coff && c < o.coff + convs[ops[i + q].conv].cout) return q;
+            }
+            return -1;
+        };
+        for (int k = 0; k < n; ++k) {
+            const Op& o = ops[i + k];
+            Op::PwStage& st = ch.pws[k];
+            for (const Seg& sg : o.in) {
+                const View& v = sg.v;
+                for (int c = v.coff; c < v.coff + v.C;) {
+                    const int q = producer(k, v.t, c);
+                    int c1 = c + 8;
+                    while (c1 < v.coff + v.C && producer(k, v.t, c1) == q) c1 += 8;
+                    Op::PwRun r;
+                    r.stage = q;
+                    r.nch = c1 - c;
+                    r.coff = q >= 0 ? c - ops[i + q].out.coff : c;
+                    if (r.nch % 128) return false;
+                    if (q < 0) {   // a global view: one prologue load per distinct view
+                        View g;
+                        g.t = v.t; g.coff = c; g.C = r.nch;
+                        int li = -1;
+                        for (size_t z = 0; z < ch.pwl.size(); ++z)
+                            if (ch.pwl[z].t == g.t && ch.pwl[z].coff == g.coff && ch.pwl[z].C == g.C) li = (int)z;
+                        if (li < 0) {
+                            li = (int)ch.pwl.size();
+                            ch.pwl.push_back(g);
+                        }
+                        r.load = li;
+                    } else {
+                        ch.pws[q].keep = true;
+                    }
+                    st.runs.push_back(r);
+                    c = c1;
+                }
+            }
+            if ((int)st.runs.size() > PWC_MAX_RUNS) return false;
+            if (o.has_res) {
+                const int cout = convs[o.conv].cout;
+                const int q = producer(k, o.res.t, o.res.coff);
+                for (int c = o.res.coff; c < o.res.coff + cout; c += 8)
+                    if (producer(k, o.res.t, c) != q) return false;
+                st.res_stage = q;
+                if (q >= 0) {
+                    st.res_coff = o.res.coff - ops[i + q].out.coff;
+                    ch.pws[q].keep = true;
+                } else {   // a global residual also comes in by the prologue (no VGPR load in the epilogue)
+                    View g;
+                    g.t = o.res.t; g.coff = o.res.coff; g.C = cout;
+                    int li = -1;
+                    for (size_t z = 0; z < ch.pwl.size(); ++z)
+                        if (ch.pwl[z].t == g.t && ch.pwl[z].coff == g.coff && ch.pwl[z].C == g.C) li = (int)z;
+                    if (li < 0) {
+                        li = (int)ch.pwl.size();
+                        ch.pwl.push_back(g);
+                    }
+                    st.res_load = li;
+                }
+            }
+        }
+        if ((int)ch.pwl.size() > PWC_MAX_LOADS) return false;
+        // LDS: the kept stage outputs (pixel stride cout + 8), then the loads (stride C + 8,
+        // whole 1 KB LDS-DMA instructions)
+        auto layout = [&](int P) {
+            int off = 0;
+            for (int k = 0; k < n; ++k) {
+                Op::PwStage& st = ch.pws[k];
+                st.lds = -1;
+                if (!st.keep) continue;
+                st.lds = off;
+                off += (P * (convs[ops[i + k].conv].cout + 8) * 2 + 15) & ~15;
+            }
+            ch.pwl_lds.assign(ch.pwl.size(), 0);
+            for (size_t z = 0; z < ch.pwl.size(); ++z) {
+                off = (off + 1023) & ~1023;
+                ch.pwl_lds[z] = off;
+                off += (P * (ch.pwl[z].C + 8) * 2 + 1023) & ~1023;
+            }
+            off = (off + 1023) & ~1023;
+            return off + 1024;   // the weight warm-up DMAs' sink (pw_chain)
+        };
+        int P = 64, lds = layout(64);
+        if (lds > 160 * 1024) {
+            P = 32;
+            lds = layout(32);
+        }
+        if (lds > 160 * 1024) return false;
+        ch.pwP = P;
+        ch.pwLds = lds;
+        for (int k = 0; k < n; ++k) ch.alts.push_back((int)(i + k));
+        ch.label = ops[i].label + " +" + std::to_string(n - 1);
+        ch.out = ops[e - 1].out;
+        // insert at e: op indices >= e move up by one
+        for (auto& o : ops) {
+            if (o.alt0 >= (int)e) o.alt0++;
+            if (o.alt1 >= (int)e) o.alt1++;
+            for (int& k : o.alts)
+                if (k >= (int)e) k++;
+        }
+        ops.insert(ops.begin() + e, ch);
+        return true;
     }
     // a dense conv with a single unsegmented input and no op of its own (fused ops)
     int new_dense_conv(const std::string& name, int cin, int cout, int k, int has_bias, int act) {
@@ -1323,6 +1485,65 @@ struct Net {
         (void)hipEventDestroy(e1);
     }
 
+    PwChainArgs pw_chain_args(const Op& op, int B, int H, int W) {
+        PwChainArgs a{};
+        const int lv = tensors[op.out.t].level;
+        a.M = (long long)B * (H >> lv) * (W >> lv);
+        a.P = op.pwP;
+        a.nst = (int)op.pws.size();
+        a.nload = (int)op.pwl.size();
+        a.sink = op.pwLds - 1024;
+        a.zero = zero_dev;
+        for (int z = 0; z < a.nload; ++z) {
+            PwcLoad& L = a.ld[z];
+            L.g = ptr(op.pwl[z]);
+            L.ldg = ldc(op.pwl[z]);
+            L.lds = op.pwl_lds[z];
+            L.nchunk = op.pwl[z].C / 8;
+        }
+        for (int k = 0; k < a.nst; ++k) {
+            const Op& o = ops[op.alts[k]];
+            const ConvDesc& d = convs[o.conv];
+            const Op::PwStage& ps = op.pws[k];
+            PwcStage& st = a.st[k];
+            st.K = d.K;
+            st.N = d.cout;
+            st.act = d.act;
+            st.nrun = (int)ps.runs.size();
+            for (int r = 0; r < st.nrun; ++r) {
+                const Op::PwRun& pr = ps.runs[r];
+                PwcRun& R = st.run[r];
+                R.nkb = pr.nch / 16;
+                if (pr.stage >= 0) {
+                    const int ld = convs[ops[op.alts[pr.stage]].conv].cout + 8;
+                    R.lds = op.pws[pr.stage].lds + pr.coff * 2;
+                    R.ld = ld;
+                } else {
+                    R.lds = op.pwl_lds[pr.load];
+                    R.ld = op.pwl[pr.load].C + 8;
+                }
+            }
+            st.w = d.w_dev;
+            st.wld = d.Kp;
+            st.bias = d.b_dev;
+            st.res_lds = -1;
+            if (o.has_res) {
+                if (ps.res_stage >= 0) {
+                    st.res_lds = op.pws[ps.res_stage].lds + ps.res_coff * 2;
+                    st.res_ldl = convs[ops[op.alts[ps.res_stage]].conv].cout + 8;
+                } else {
+                    st.res_lds = op.pwl_lds[ps.res_load];
+                    st.res_ldl = op.pwl[ps.res_load].C + 8;
+                }
+            }
+            st.out = ptr(o.out);
+            st.ldo = ldc(o.out);
+            st.out_lds = ps.keep ? ps.lds : -1;
+            st.out_ldl = d.cout + 8;
+        }
+        return a;
+    }
+
     HeadClsArgs head_cls_args(const Op& op, int B, int H, int W) {
         HeadClsArgs a{};
         a.B = B;
@@ -1462,6 +1683,7 @@ struct Net {
             }
             case OP_BOXDFL: rc = launch_box_dfl(dtype, box_dfl_args(op, B, H, W), s); break;
             case OP_BOXCHAIN: rc = launch_box_chain(dtype, box_chain_args(op, B, H, W), s); break;
+            case OP_PWCHAIN: rc = launch_pw_chain(dtype, pw_chain_args(op, B, H, W), op.pwLds, s); break;
             case OP_STEM2: {
                 const ConvDesc& d = convs[op.conv];
                 Stem2Args a{};
@@ -1556,6 +1778,9 @@ struct Net {
             else
                 pl.active[i] = 0;
         }
+        for (size_t i = 0; i < ops.size(); ++i)
+            if (ops[i].kind == OP_PWCHAIN)
+                for (int k : ops[i].alts) pl.active[k] = 0;
         for (size_t i = 0; i < ops.size(); ++i) {
             if (ops[i].kind != OP_C3K) continue;
             const int lv = tensors[ops[i].out.t].level;
@@ -1660,6 +1885,7 @@ struct Net {
             case OP_STEM2: return CL_FIRST;
             case OP_C3K: return CL_C3K;
             case OP_BOXCHAIN: return CL_BOXCHAIN;
+            case OP_PWCHAIN: return CL_PWCHAIN;
         }
         return CL_CONV1;
     }
@@ -1775,6 +2001,19 @@ struct Net {
                 }
                 break;
             }
+            case OP_PWCHAIN: {
+                // the prologue's global inputs (incl. the global residuals) read once, every stage's
+                // output written (all stay materialised), each stage's weights once
+                const double n = px(tensors[op.out.t].level);
+                for (const View& v : op.pwl) bytes += n * v.C * es;
+                for (size_t k = 0; k < op.pws.size(); ++k) {
+                    const Op& o = ops[op.alts[k]];
+                    const ConvDesc& d = convs[o.conv];
+                    bytes += n * d.cout * es + (double)d.cout * d.cin * es;
+                    flops += 2.0 * n * d.cout * d.cin;
+                }
+                break;
+            }
             case OP_BOXCHAIN: {
                 // the level inputs read once, 4 box rows written, the three convs' weights once
                 for (int l = 0; l < 3; ++l) {
@@ -1848,8 +2087,35 @@ struct Net {
             case OP_DECODE:
                 for (int l = 0; l < 3; ++l) add("L" + std::to_string(l), op.lvl[l], 0, 64 + var.num_classes);
                 break;
+            case OP_PWCHAIN:
+                // per stage s<k>.in<i> / s<k>.res (inputs, read before the chain runs), then the
+                // outputs no later stage overwrites (s<k>.out)
+                for (size_t k = 0; k < op.alts.size(); ++k) {
+                    const Op& o = ops[op.alts[k]];
+                    const ConvDesc& d = convs[o.conv];
+                    const std::string p = "s" + std::to_string(k) + ".";
+                    for (size_t si = 0; si < o.in.size(); ++si) add(p + "in" + std::to_string(si), o.in[si].v, 0, d.segs[si].first);
+                    if (o.has_res) add(p + "res", o.res, 0, d.cout);
+                }
+                for (size_t k = 0; k < op.alts.size(); ++k)
+                    if (pw_final(op, (int)k)) {
+                        const Op& o = ops[op.alts[k]];
+                        add("s" + std::to_string(k) + ".out", o.out, 0, convs[o.conv].cout);
+                    }
+                break;
         }
         return r;
+    }
+    // stage k's output is not overwritten by a later stage of the chain
+    bool pw_final(const Op& op, int k) const {
+        const Op& o = ops[op.alts[k]];
+        const int c0 = o.out.coff, c1 = c0 + convs[o.conv].cout;
+        for (size_t q = k + 1; q < op.alts.size(); ++q) {
+            const Op& w = ops[op.alts[q]];
+            const int w0 = w.out.coff, w1 = w0 + convs[w.conv].cout;
+            if (w.out.t == o.out.t && w0 < c1 && c0 < w1) return false;
+        }
+        return true;
     }
     // the convs an op computes, in the op's order (-1: none in that place, e.g. tail-mode conv1)
     std::vector<int> op_convs(const Op& op) const {
@@ -1869,6 +2135,11 @@ struct Net {
                 std::vector<int> r;
                 for (int l = 0; l < 3; ++l)
                     for (int k = 0; k < 3; ++k) r.push_back(op.bxc[l][k]);
+                return r;
+            }
+            case OP_PWCHAIN: {
+                std::vector<int> r;
+                for (int k : op.alts) r.push_back(ops[k].conv);
                 return r;
             }
             case OP_SPPF: case OP_DECODE: return {};
@@ -1902,7 +2173,34 @@ struct Net {
                  ", \"W\": " + std::to_string(W >> lv) + ", \"C\": " + std::to_string(od[i].v.C) + ", \"logical\": " +
                  std::to_string(od[i].logical) + ", \"up\": " + std::to_string(od[i].up) + "}";
         }
-        s += "]}";
+        s += "]";
+        if (op.kind == OP_PWCHAIN) {
+            // per stage: its input runs in weight order (seg = input segment, off = channel within
+            // it; src = -1: that device operand, else the output of stage src from channel soff) and
+            // its residual source (-2 none, -1 the s<k>.res operand, else a stage's output)
+            s += ", \"stages\": [";
+            for (size_t k = 0; k < op.pws.size(); ++k) {
+                const Op& o = ops[op.alts[k]];
+                const Op::PwStage& ps = op.pws[k];
+                s += std::string(k ? ", " : "") + "{\"runs\": [";
+                int si = 0, soff = 0;
+                for (size_t r = 0; r < ps.runs.size(); ++r) {
+                    const Op::PwRun& pr = ps.runs[r];
+                    while (soff >= o.in[si].v.C) {
+                        soff -= o.in[si].v.C;
+                        ++si;
+                    }
+                    s += std::string(r ? ", " : "") + "{\"seg\": " + std::to_string(si) + ", \"off\": " +
+                         std::to_string(soff) + ", \"n\": " + std::to_string(pr.nch) + ", \"src\": " +
+                         std::to_string(pr.stage) + ", \"soff\": " + std::to_string(pr.stage >= 0 ? pr.coff : 0) + "}";
+                    soff += pr.nch;
+                }
+                s += "], \"res\": " + std::to_string(o.has_res ? ps.res_stage : -2) + ", \"res_off\": " +
+                     std::to_string(ps.res_coff) + ", \"final\": " + std::to_string(pw_final(op, (int)k) ? 1 : 0) + "}";
+            }
+            s += "]";
+        }
+        s += "}";
         return s;
     }
     // the active ops in [first, last) of the forward at (B, H, W), launched eagerly on s

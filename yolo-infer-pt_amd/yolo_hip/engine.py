@@ -17,7 +17,7 @@ from ._lib import YhVariant, check, lib
 _DTYPES = {torch.float32: _lib.YH_F32, torch.float16: _lib.YH_F16, torch.bfloat16: _lib.YH_BF16}
 
 OP_CLASSES = ("conv3x3", "conv1x1", "stem", "dwconv", "sppf", "attention", "decode", "head_cls", "box_dfl", "c3k2",
-              "c3k", "box_chain")
+              "c3k", "box_chain", "pw_chain")
 
 
 def dtype_code(dtype):
