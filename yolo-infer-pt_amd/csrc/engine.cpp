@@ -1778,9 +1778,22 @@ struct Net {
             else
                 pl.active[i] = 0;
         }
-        for (size_t i = 0; i < ops.size(); ++i)
-            if (ops[i].kind == OP_PWCHAIN)
+        // a pointwise chain reads every stage's weights once per workgroup: kept where that is at
+        // most 160 MB per launch (v11_n b32: 52-90 MB, 104 -> 77 us for its three chains),
+        // per-layer launches above (v11_s b64 1.4 GB: the chains ran 2.2x slower,
+        // profiles/r05_pw_chain_configs.txt)
+        for (size_t i = 0; i < ops.size(); ++i) {
+            if (ops[i].kind != OP_PWCHAIN) continue;
+            const int lv = tensors[ops[i].out.t].level;
+            const long long M = (long long)B * (H >> lv) * (W >> lv);
+            const double grid = (double)((M + ops[i].pwP - 1) / ops[i].pwP);
+            double wb = 0;
+            for (int k : ops[i].alts) wb += (double)convs[ops[k].conv].cout * convs[ops[k].conv].K * es;
+            if (wb * grid <= 160e6)
                 for (int k : ops[i].alts) pl.active[k] = 0;
+            else
+                pl.active[i] = 0;
+        }
         for (size_t i = 0; i < ops.size(); ++i) {
             if (ops[i].kind != OP_C3K) continue;
             const int lv = tensors[ops[i].out.t].level;
