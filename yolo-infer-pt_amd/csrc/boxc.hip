@@ -351,8 +351,7 @@ __device__ __forceinline__ void bx_body(const BoxChainArgs& A, int li, char* sm)
             const float x2 = ax + dr, y2 = ay + db;
             const float r0 = h ? (x2 - x1) * st : (x1 + x2) / 2.0f * st;
             const float r1 = h ? (y2 - y1) * st : (y1 + y2) / 2.0f * st;
-            T* col = reinterpret_cast<T*>(const_cast<void*>(A.io[1])) + ((long long)n * (4 + A.nc) + 2 * h) * A.A + V.aoff +
-                     gy * W + gx;
+            const gptr<T> col = io_global<T>(A.io[1]) + ((long long)n * (4 + A.nc) + 2 * h) * A.A + V.aoff + gy * W + gx;
             col[0] = fromf<T>(r0);
             col[A.A] = fromf<T>(r1);
         }

@@ -113,6 +113,21 @@ template <> struct Mma<float> {
     }
 };
 
+// The caller's output tensor reached through io[] (a pointer loaded from device memory, so the
+// compiler cannot infer its address space): as a global pointer its stores are global_store,
+// counted in vmcnt only. Through the generic pointer they are flat stores, which also count in
+// lgkmcnt - every later LDS wait of the wave would then wait for them to reach memory - and the
+// pointer itself is re-loaded (waiting on vmcnt(0)) at every store it may alias.
+template <typename T> using gptr = __attribute__((address_space(1))) T*;
+template <typename T> __device__ __forceinline__ gptr<T> io_global(const void* p) { return (gptr<T>)(const_cast<void*>(p)); }
+typedef unsigned int u32x4v __attribute__((ext_vector_type(4)));
+template <typename T>
+__device__ __forceinline__ void st_chunk(gptr<T> p, const Chunk<T>& c) {
+    const gptr<u32x4v> q = (gptr<u32x4v>)p;
+#pragma unroll
+    for (int i = 0; i < (int)(sizeof(T) / 2); ++i) q[i] = __builtin_bit_cast(u32x4v, c.v[i]);
+}
+
 // XCD-aware bijective remap of a 1-D block id: blocks b and b+8 share an XCD
 // (round-robin dispatch), so give each XCD a contiguous range of logical ids.
 __device__ __forceinline__ int xcd_remap(int bid, int nwg) {

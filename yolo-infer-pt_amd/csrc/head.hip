@@ -459,6 +459,7 @@ __device__ __forceinline__ void hc_body(const HeadClsArgs& A, int li, char* hsm)
     // 6. pw3: P2 (R1) -> class logits in the head tensor, or (direct mode) their sigmoid in
     //    the caller's y, one row per class (the decode's class part: logit rounded first)
     T* y = reinterpret_cast<T*>(V.y);
+    const gptr<T> yio = A.io ? io_global<T>(A.io[1]) : nullptr;   // loaded once (see io_global)
     auto pw3 = [&](auto store) {
         if constexpr (P2 > 0)
             hc_pw_run<T, NK2, P2>(R1, L.SM, TH * TW, reinterpret_cast<const T*>(V.pw3w), V.pw3ld, QB3, A.nc, false, A3,
@@ -471,8 +472,7 @@ __device__ __forceinline__ void hc_body(const HeadClsArgs& A, int li, char* hsm)
             const int r = hc_q(px, dtw), cc = px - r * TW;
             const int gh = h0 + r, gw = w0 + cc;
             if ((unsigned)gh < (unsigned)H && (unsigned)gw < (unsigned)W) {
-                T* col = reinterpret_cast<T*>(const_cast<void*>(A.io[1])) +
-                         ((long long)n * (4 + A.nc) + 4 + co) * A.A + V.aoff + gh * W + gw;
+                const gptr<T> col = yio + ((long long)n * (4 + A.nc) + 4 + co) * A.A + V.aoff + gh * W + gw;
                 const T* o = reinterpret_cast<const T*>(&v);
 #pragma unroll
                 for (int e = 0; e < 4; ++e) col[(long long)e * A.A] = fromf<T>(hx_div(1.0f, 1.0f + hx_exp(-tof(o[e]))));
@@ -550,7 +550,7 @@ __device__ __forceinline__ void bd_body(const BoxDflArgs& A, int li) {
     uint4 bf[BOX_DFL_TPW][NK];   // every tile's loads in flight at once (HBM latency)
 #pragma unroll
     for (int t = 0; t < BOX_DFL_TPW; ++t) load_b(tile0 + t, bf[t]);
-    T* yb = reinterpret_cast<T*>(const_cast<void*>(A.io[1]));
+    const gptr<T> yb = io_global<T>(A.io[1]);
 #pragma unroll
     for (int t = 0; t < BOX_DFL_TPW; ++t) {
         const long long tt = tile0 + t;
@@ -590,7 +590,7 @@ __device__ __forceinline__ void bd_body(const BoxDflArgs& A, int li) {
             const float x2 = ax + dr, y2 = ay + db;
             const float r0 = h ? (x2 - x1) * st : (x1 + x2) / 2.0f * st;
             const float r1 = h ? (y2 - y1) * st : (y1 + y2) / 2.0f * st;
-            T* col = yb + ((long long)n * (4 + A.nc) + 2 * h) * A.A + V.aoff + loc;
+            const gptr<T> col = yb + ((long long)n * (4 + A.nc) + 2 * h) * A.A + V.aoff + loc;
             col[0] = fromf<T>(r0);
             col[A.A] = fromf<T>(r1);
         }

@@ -298,6 +298,16 @@ __device__ __forceinline__ s16x4 lds_tr16(const void* p) {
 #endif
 }
 
+// 16 bytes from p when ok, else zeros: a branch around the load. (The `ok ? *p : zero`
+// form lets the compiler load through a select of p and a stack zero, a flat load - counted
+// in lgkmcnt as well as vmcnt - even when p is global or LDS.)
+template <typename P>
+__device__ __forceinline__ uint4 ld16_if(bool ok, const P* p) {
+    uint4 v = make_uint4(0, 0, 0, 0);
+    if (ok) v = *reinterpret_cast<const uint4*>(p);
+    return v;
+}
+
 template <typename T>
 __global__ __launch_bounds__(256) void psa_attention_mfma(const AttnArgs p) {
     __shared__ __attribute__((aligned(16))) T vlds[4][16 * DH];
@@ -309,7 +319,7 @@ __global__ __launch_bounds__(256) void psa_attention_mfma(const AttnArgs p) {
     const T* base = reinterpret_cast<const T*>(p.qkv) + (long long)n * p.T * p.ldq + head * (2 * DK + DH);
     const uint4 z4 = make_uint4(0, 0, 0, 0);
     const int q = q0 + li;
-    const uint4 qf = q < p.T ? *reinterpret_cast<const uint4*>(base + (long long)q * p.ldq + 8 * g) : z4;
+    const uint4 qf = ld16_if(q < p.T, base + (long long)q * p.ldq + 8 * g);
     f32x4 o[4];
 #pragma unroll
     for (int t = 0; t < 4; ++t) o[t] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -317,12 +327,12 @@ __global__ __launch_bounds__(256) void psa_attention_mfma(const AttnArgs p) {
     T* vl = vlds[wave];
     for (int kb = 0; kb < p.T; kb += 16) {
         const int key = kb + li;
-        const uint4 kf = key < p.T ? *reinterpret_cast<const uint4*>(base + (long long)key * p.ldq + DK + 8 * g) : z4;
+        const uint4 kf = ld16_if(key < p.T, base + (long long)key * p.ldq + DK + 8 * g);
         uint4 vv[2];
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
             const int c = lane + 64 * h, kr = c >> 3, ch = c & 7;
-            vv[h] = (kb + kr < p.T) ? *reinterpret_cast<const uint4*>(base + (long long)(kb + kr) * p.ldq + 2 * DK + ch * 8) : z4;
+            vv[h] = ld16_if((kb + kr < p.T), base + (long long)(kb + kr) * p.ldq + 2 * DK + ch * 8);
         }
         f32x4 s = f32x4{0.f, 0.f, 0.f, 0.f};
         Mma<T>::step(s, &kf, &qf);
@@ -403,7 +413,7 @@ __global__ __launch_bounds__(64 * AT_NW) void psa_attention_lds(const AttnArgs p
     const uint4 z4 = make_uint4(0, 0, 0, 0);
     const int q = q0 + li;
     const bool qwave = q0 < p.T;   // wave-uniform: waves past the last query block only load
-    const uint4 qf = (qwave && q < p.T) ? *reinterpret_cast<const uint4*>(base + (long long)q * p.ldq + 8 * g) : z4;
+    const uint4 qf = ld16_if((qwave && q < p.T), base + (long long)q * p.ldq + 8 * g);
     f32x4 o[4];
 #pragma unroll
     for (int t = 0; t < 4; ++t) o[t] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -416,7 +426,7 @@ __global__ __launch_bounds__(64 * AT_NW) void psa_attention_lds(const AttnArgs p
         const int nk16 = (nk + 15) & ~15;
         for (int i = threadIdx.x; i < nk16 * 12; i += 64 * AT_NW) {
             const int r = i / 12, c = i - r * 12;
-            const uint4 v = r < nk ? *reinterpret_cast<const uint4*>(base + (long long)(k0 + r) * p.ldq + DK + 8 * c) : z4;
+            const uint4 v = ld16_if(r < nk, base + (long long)(k0 + r) * p.ldq + DK + 8 * c);
             if (c < 4) *reinterpret_cast<uint4*>(klds + r * DK + 8 * c) = v;
             else *reinterpret_cast<uint4*>(vlds + r * AT_VS + 8 * (c - 4)) = v;
         }
@@ -424,7 +434,7 @@ __global__ __launch_bounds__(64 * AT_NW) void psa_attention_lds(const AttnArgs p
         if (!qwave) continue;
         for (int kb = 0; kb < nk; kb += 16) {
             const int key = kb + li;
-            const uint4 kf = key < nk ? *reinterpret_cast<const uint4*>(klds + key * DK + 8 * g) : z4;
+            const uint4 kf = ld16_if(key < nk, klds + key * DK + 8 * g);
             f32x4 s = f32x4{0.f, 0.f, 0.f, 0.f};
             Mma<T>::step(s, &kf, &qf);
             float sv[4], mx = -INFINITY;
@@ -506,7 +516,7 @@ __global__ __launch_bounds__(64 * AF_NW) void psa_attention_full(const AttnArgs 
     // missing keys), the head's positional weights and bias
     for (int i = threadIdx.x; i < t16 * 12; i += 64 * AF_NW) {
         const int r = i / 12, c = i - r * 12;
-        const uint4 v = r < p.T ? *reinterpret_cast<const uint4*>(base + (long long)r * p.ldq + DK + 8 * c) : z4;
+        const uint4 v = ld16_if(r < p.T, base + (long long)r * p.ldq + DK + 8 * c);
         if (c < 4) *reinterpret_cast<uint4*>(klds + r * DK + 8 * c) = v;
         else *reinterpret_cast<uint4*>(vlds + r * AT_VS + 8 * (c - 4)) = v;
     }
@@ -516,14 +526,14 @@ __global__ __launch_bounds__(64 * AF_NW) void psa_attention_full(const AttnArgs 
     const int nqb = (p.T + 15) >> 4;
     for (int qb = split * AF_NW + wave; qb < nqb; qb += qs * AF_NW) {   // wave-uniform
         const int q = qb * 16 + li;
-        const uint4 qf = q < p.T ? *reinterpret_cast<const uint4*>(base + (long long)q * p.ldq + 8 * g) : z4;
+        const uint4 qf = ld16_if(q < p.T, base + (long long)q * p.ldq + 8 * g);
         f32x4 o[4];
 #pragma unroll
         for (int t = 0; t < 4; ++t) o[t] = f32x4{0.f, 0.f, 0.f, 0.f};
         float mrun = -INFINITY, lrun = 0.f;
         for (int kb = 0; kb < p.T; kb += 16) {
             const int key = kb + li;
-            const uint4 kf = key < p.T ? *reinterpret_cast<const uint4*>(klds + key * DK + 8 * g) : z4;
+            const uint4 kf = ld16_if(key < p.T, klds + key * DK + 8 * g);
             f32x4 s = f32x4{0.f, 0.f, 0.f, 0.f};
             Mma<T>::step(s, &kf, &qf);
             float sv[4], mx = -INFINITY;
@@ -676,7 +686,7 @@ __global__ __launch_bounds__(256) void head_decode(const DecodeArgs p) {
     const int n = blockIdx.y, a0 = p.a_lo + blockIdx.x * 256;
     const int a = a0 + threadIdx.x;
     const bool live = a < p.A;
-    T* yimg = reinterpret_cast<T*>(const_cast<void*>(p.io[1])) + (long long)n * (4 + p.nc) * p.A;
+    const gptr<T> yimg = io_global<T>(p.io[1]) + (long long)n * (4 + p.nc) * p.A;
     auto put = [&](int r, float v) {
         if constexpr (ROWS) tile[r * 256 + threadIdx.x] = fromf<T>(v);
         else if (live) yimg[(long long)r * p.A + a] = fromf<T>(v);
@@ -751,7 +761,7 @@ __global__ __launch_bounds__(256) void head_decode(const DecodeArgs p) {
             const int a8 = a0 + 8 * k;
             if (a8 >= p.A) continue;
             const T* srow = tile + r * 256 + 8 * k;
-            T* drow = yimg + (long long)r * p.A + a8;
+            const gptr<T> drow = yimg + (long long)r * p.A + a8;
             if (a8 + 8 <= p.A) {
                 st_chunk(drow, ld_chunk(srow));
             } else {
@@ -859,7 +869,7 @@ __global__ __launch_bounds__(256, 2) void head_decode_lds(const DecodeArgs p) {
         for (int e = 0; e < 8; ++e) tile[(4 + 8 * c + e) * DEC_A + tid] = fromf<T>(dv<T>(1.0f, 1.0f + ex<T>(-f[e])));
     }
     __syncthreads();
-    T* yimg = reinterpret_cast<T*>(const_cast<void*>(p.io[1])) + (long long)n * (4 + p.nc) * p.A;
+    const gptr<T> yimg = io_global<T>(p.io[1]) + (long long)n * (4 + p.nc) * p.A;
     constexpr int R0 = BOX ? 0 : 4;
     const int rows = 4 + p.nc - R0;
     for (int c = tid; c < rows * (DEC_A / 8); c += 256) {
@@ -867,7 +877,7 @@ __global__ __launch_bounds__(256, 2) void head_decode_lds(const DecodeArgs p) {
         const int a8 = a0 + 8 * k;
         if (a8 >= p.A) continue;
         const T* srow = tile + r * DEC_A + 8 * k;
-        T* drow = yimg + (long long)r * p.A + a8;
+        const gptr<T> drow = yimg + (long long)r * p.A + a8;
         if (a8 + 8 <= p.A) st_chunk(drow, ld_chunk(srow));
         else for (int e = 0; a8 + e < p.A; ++e) drow[e] = srow[e];
     }
