@@ -190,24 +190,28 @@ def test_attention_full_kernel_equals_chunked_kernel_and_pe_add(gpu, variant, dt
     """misc.hip psa_attention_full (one workgroup per (image, head), the whole K / V in LDS, the
     positional term added in the epilogue) is bit-identical to the chunked kernel followed by
     pe_add (YH_ATTN_FULL=0), including partial key blocks (224: 49 tokens) and several heads
-    (m: 4 heads at 480 -> 225 tokens)."""
+    (m: 4 heads at 480 -> 225 tokens). Both workgroup shapes of the full kernel: these small
+    batches pick 8 waves with one 16-query block per wave, YH_ATTN_NW=16 forces the 16-wave shape
+    the large batches use (YH_ATTN_QS=1: several query blocks per wave)."""
     model = make_model(variant)
     x = synth.synth_scenes(batch, size, size, seed=34).to(gpu, dtype)
     ys = []
-    for v in ("0", "1"):
-        old = os.environ.get("YH_ATTN_FULL")
-        os.environ["YH_ATTN_FULL"] = v
+    for env in ({"YH_ATTN_FULL": "0"}, {"YH_ATTN_FULL": "1"}, {"YH_ATTN_FULL": "1", "YH_ATTN_NW": "16", "YH_ATTN_QS": "1"}):
+        old = {k: os.environ.get(k) for k in env}
+        os.environ.update(env)
         try:
             eng = _engine(model, dtype, gpu, True)
             ys.append(eng.forward(x).clone())
             torch.cuda.synchronize()
         finally:
-            if old is None:
-                del os.environ["YH_ATTN_FULL"]
-            else:
-                os.environ["YH_ATTN_FULL"] = old
+            for k, v in old.items():
+                if v is None:
+                    del os.environ[k]
+                else:
+                    os.environ[k] = v
     assert torch.isfinite(ys[0].float()).all()
-    assert torch.equal(ys[0], ys[1]), (ys[0].float() - ys[1].float()).abs().max().item()
+    for y in ys[1:]:
+        assert torch.equal(ys[0], y), (ys[0].float() - y.float()).abs().max().item()
 
 
 @pytest.mark.parametrize("variant,dtype,batch,size", [("n", torch.bfloat16, 4, 640), ("s", torch.float16, 2, 320),

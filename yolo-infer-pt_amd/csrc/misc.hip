@@ -298,6 +298,32 @@ __device__ __forceinline__ s16x4 lds_tr16(const void* p) {
 #endif
 }
 
+// Reductions over the four 16-lane rows of a wave (lanes l, l ^ 16, l ^ 32, l ^ 48) by gfx950's
+// row swaps (v_permlane16_swap / v_permlane32_swap: VALU, no LDS round trip as a ds_bpermute
+// shuffle has). Each step combines a lane's value with its xor-16 / xor-32 partner's, the two
+// operands in a fixed order; max and + commute, so every lane gets the bits the shuffle form
+// (own value op partner's) gives.
+__device__ __forceinline__ float rows4_max(float x) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+    x = fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+    const auto t = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+    return fmaxf(__uint_as_float(t[0]), __uint_as_float(t[1]));
+#else
+    return x;
+#endif
+}
+__device__ __forceinline__ float rows4_sum(float x) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+    x = __uint_as_float(r[0]) + __uint_as_float(r[1]);
+    const auto t = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+    return __uint_as_float(t[0]) + __uint_as_float(t[1]);
+#else
+    return x;
+#endif
+}
+
 // 16 bytes from p when ok, else zeros: a branch around the load. (The `ok ? *p : zero`
 // form lets the compiler load through a select of p and a stack zero, a flat load - counted
 // in lgkmcnt as well as vmcnt - even when p is global or LDS.)
@@ -342,8 +368,7 @@ __global__ __launch_bounds__(256) void psa_attention_mfma(const AttnArgs p) {
             sv[r] = (kb + 4 * g + r < p.T) ? s[r] * p.scale : -INFINITY;
             mx = fmaxf(mx, sv[r]);
         }
-        mx = fmaxf(mx, __shfl_xor(mx, 16));
-        mx = fmaxf(mx, __shfl_xor(mx, 32));
+        mx = rows4_max(mx);
         const float mnew = fmaxf(mrun, mx);
         const float corr = __expf(mrun - mnew);
         float ps = 0.f;
@@ -354,8 +379,7 @@ __global__ __launch_bounds__(256) void psa_attention_mfma(const AttnArgs p) {
             pb[r] = __builtin_bit_cast(short, fromf<T>(pr));
             ps += pr;
         }
-        ps += __shfl_xor(ps, 16);
-        ps += __shfl_xor(ps, 32);
+        ps = rows4_sum(ps);
         lrun = lrun * corr + ps;
         mrun = mnew;
 #pragma unroll
@@ -443,8 +467,7 @@ __global__ __launch_bounds__(64 * AT_NW) void psa_attention_lds(const AttnArgs p
                 sv[r] = (kb + 4 * g + r < nk) ? s[r] * p.scale : -INFINITY;
                 mx = fmaxf(mx, sv[r]);
             }
-            mx = fmaxf(mx, __shfl_xor(mx, 16));
-            mx = fmaxf(mx, __shfl_xor(mx, 32));
+            mx = rows4_max(mx);
             const float mnew = fmaxf(mrun, mx);
             const float corr = __expf(mrun - mnew);
             float ps = 0.f;
@@ -455,8 +478,7 @@ __global__ __launch_bounds__(64 * AT_NW) void psa_attention_lds(const AttnArgs p
                 pb[r] = __builtin_bit_cast(short, fromf<T>(pr));
                 ps += pr;
             }
-            ps += __shfl_xor(ps, 16);
-            ps += __shfl_xor(ps, 32);
+            ps = rows4_sum(ps);
             lrun = lrun * corr + ps;
             mrun = mnew;
 #pragma unroll
@@ -489,13 +511,13 @@ __global__ __launch_bounds__(64 * AT_NW) void psa_attention_lds(const AttnArgs p
 // arithmetic for its 16-query blocks in the same key order, rounds the output as that kernel
 // stores it, then adds pe_b and the 3 x 3 taps in pe_add's order with pe_add's fmaf chain:
 // the result is bit-identical to psa_attention_mfma / psa_attention_lds followed by pe_add.
-constexpr int AF_NW = 16, AF_TMAX = 640;
+constexpr int AF_NW = 16, AF_TMAX = 640, AF_LB = 8;
 __host__ __device__ inline int af_lds_bytes(int T) {
     const int t16 = (T + 15) & ~15;
     return t16 * (DK + AT_VS) * 2 + 10 * DH * 4;
 }
-template <typename T>
-__global__ __launch_bounds__(64 * AF_NW) void psa_attention_full(const AttnArgs p, int B) {
+template <typename T, int NW>
+__global__ __launch_bounds__(64 * NW) void psa_attention_full(const AttnArgs p, int B) {
     extern __shared__ __attribute__((aligned(16))) char afs[];
     const int t16 = (p.T + 15) & ~15;
     T* klds = reinterpret_cast<T*>(afs);
@@ -514,36 +536,55 @@ __global__ __launch_bounds__(64 * AF_NW) void psa_attention_full(const AttnArgs 
     const uint4 z4 = make_uint4(0, 0, 0, 0);
     // every token row [k(32) | v(64)] once (zeros past the last token: the per-wave kernel's
     // missing keys), the head's positional weights and bias
-    for (int i = threadIdx.x; i < t16 * 12; i += 64 * AF_NW) {
-        const int r = i / 12, c = i - r * 12;
-        const uint4 v = ld16_if(r < p.T, base + (long long)r * p.ldq + DK + 8 * c);
-        if (c < 4) *reinterpret_cast<uint4*>(klds + r * DK + 8 * c) = v;
-        else *reinterpret_cast<uint4*>(vlds + r * AT_VS + 8 * (c - 4)) = v;
+    // (batches of AF_LB loads in flight per thread, then their LDS stores: a load-store pair per
+    // iteration would put one memory round trip per iteration on the prologue's critical path)
+    for (int i0 = threadIdx.x; i0 < t16 * 12; i0 += AF_LB * 64 * NW) {
+        uint4 v[AF_LB];
+#pragma unroll
+        for (int u = 0; u < AF_LB; ++u) {
+            const int i = i0 + u * 64 * NW, r = i / 12, c = i - r * 12;
+            v[u] = ld16_if(i < t16 * 12 && r < p.T, base + (long long)r * p.ldq + DK + 8 * c);
+        }
+#pragma unroll
+        for (int u = 0; u < AF_LB; ++u) {
+            const int i = i0 + u * 64 * NW, r = i / 12, c = i - r * 12;
+            if (i >= t16 * 12) break;
+            if (c < 4) *reinterpret_cast<uint4*>(klds + r * DK + 8 * c) = v[u];
+            else *reinterpret_cast<uint4*>(vlds + r * AT_VS + 8 * (c - 4)) = v[u];
+        }
     }
-    for (int i = threadIdx.x; i < 10 * DH; i += 64 * AF_NW)
+    for (int i = threadIdx.x; i < 10 * DH; i += 64 * NW)
         pew[i] = i < 9 * DH ? p.pe_w[(i / DH) * C + head * DH + (i % DH)] : p.pe_b[head * DH + i - 9 * DH];
     __syncthreads();
     const int nqb = (p.T + 15) >> 4;
-    for (int qb = split * AF_NW + wave; qb < nqb; qb += qs * AF_NW) {   // wave-uniform
+    for (int qb = split * NW + wave; qb < nqb; qb += qs * NW) {   // wave-uniform
         const int q = qb * 16 + li;
         const uint4 qf = ld16_if(q < p.T, base + (long long)q * p.ldq + 8 * g);
         f32x4 o[4];
 #pragma unroll
         for (int t = 0; t < 4; ++t) o[t] = f32x4{0.f, 0.f, 0.f, 0.f};
         float mrun = -INFINITY, lrun = 0.f;
+        // K rows past the last token are zeros up to t16; reads past t16 (the block after the
+        // last) are clamped: their scores are never used
+        const T* kp = klds + 8 * g;
+        uint4 kf = *reinterpret_cast<const uint4*>(kp + min(li, t16 - 1) * DK);
         for (int kb = 0; kb < p.T; kb += 16) {
-            const int key = kb + li;
-            const uint4 kf = ld16_if(key < p.T, klds + key * DK + 8 * g);
             f32x4 s = f32x4{0.f, 0.f, 0.f, 0.f};
             Mma<T>::step(s, &kf, &qf);
+            // the next block's K fragment and this block's V fragments: LDS reads issued ahead
+            // of the softmax chain they do not depend on
+            kf = *reinterpret_cast<const uint4*>(kp + min(kb + 16 + li, t16 - 1) * DK);
+            const int kr = kb + 4 * g + (li >> 2);
+            s16x4 va[4];
+#pragma unroll
+            for (int t = 0; t < 4; ++t) va[t] = lds_tr16(vlds + kr * AT_VS + 16 * t + 4 * (li & 3));
             float sv[4], mx = -INFINITY;
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 sv[r] = (kb + 4 * g + r < p.T) ? s[r] * p.scale : -INFINITY;
                 mx = fmaxf(mx, sv[r]);
             }
-            mx = fmaxf(mx, __shfl_xor(mx, 16));
-            mx = fmaxf(mx, __shfl_xor(mx, 32));
+            mx = rows4_max(mx);
             const float mnew = fmaxf(mrun, mx);
             const float corr = __expf(mrun - mnew);
             float ps = 0.f;
@@ -554,18 +595,13 @@ __global__ __launch_bounds__(64 * AF_NW) void psa_attention_full(const AttnArgs 
                 pb[r] = __builtin_bit_cast(short, fromf<T>(pr));
                 ps += pr;
             }
-            ps += __shfl_xor(ps, 16);
-            ps += __shfl_xor(ps, 32);
+            ps = rows4_sum(ps);
             lrun = lrun * corr + ps;
             mrun = mnew;
 #pragma unroll
             for (int t = 0; t < 4; ++t) o[t] *= corr;
-            const int kr = kb + 4 * g + (li >> 2);
 #pragma unroll
-            for (int t = 0; t < 4; ++t) {
-                s16x4 a = lds_tr16(vlds + kr * AT_VS + 16 * t + 4 * (li & 3));
-                o[t] = Mma16<T>::step(a, pb, o[t]);
-            }
+            for (int t = 0; t < 4; ++t) o[t] = Mma16<T>::step(va[t], pb, o[t]);
         }
         if (q >= p.T) continue;
         const float inv = 1.0f / lrun;
@@ -644,17 +680,37 @@ int launch_attention_t(const AttnArgs& a, int B, hipStream_t s) {
         if (a.T <= AF_TMAX && a.Ws > 0 && a.Hs * a.Ws == a.T && !(ef && atoi(ef) == 0)) {
             static bool attr = false;
             if (!attr) {
-                (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&psa_attention_full<T>),
+                (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&psa_attention_full<T, 16>),
+                                          hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+                (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&psa_attention_full<T, 8>),
                                           hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
                 attr = true;
             }
-            // YH_ATTN_QS: workgroups per (image, head) (each stages the whole K / V; default 2:
-            // at 1 a batch of 32 ran on 64 workgroups, 39 vs 27 us per forward)
+            // Every wave runs one 16-query block's serial chain over all key blocks, so the launch
+            // lasts about one chain when each wave has at most one block and every workgroup a CU
+            // of its own (one fits per CU: the K / V staging takes ~86 KB of LDS). Default: 8-wave
+            // workgroups, ceil(blocks / 8) per (image, head), when those fit the CUs in one round
+            // (v11_n, batch 32: 256 workgroups, 20 us); else 16-wave ones, two per (image, head)
+            // (27-28 us there; at one, 64 workgroups, 39 us). YH_ATTN_NW (8 / 16) and YH_ATTN_QS
+            // (workgroups per (image, head)) override.
+            static int ncu = 0;
+            if (!ncu) {
+                int dev = 0;
+                (void)hipGetDevice(&dev);
+                if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0)
+                    ncu = 256;
+            }
+            const int nqb = (a.T + 15) >> 4, pairs = a.heads * B, q8 = (nqb + 7) / 8;
+            const char* ew = getenv("YH_ATTN_NW");
+            const int nw = ew ? (atoi(ew) == 8 ? 8 : AF_NW) : (pairs * q8 <= ncu ? 8 : AF_NW);
             const char* eq = getenv("YH_ATTN_QS");
-            const int nqb = (a.T + 15) >> 4;
-            const int qs = std::max(1, std::min(eq ? atoi(eq) : 2, (nqb + AF_NW - 1) / AF_NW));
-            hipLaunchKernelGGL((psa_attention_full<T>), dim3((unsigned)(a.heads * B * qs)), dim3(64 * AF_NW),
-                               af_lds_bytes(a.T), s, a, B);
+            const int qs = std::max(1, std::min(eq ? atoi(eq) : (nw == 8 ? q8 : 2), (nqb + nw - 1) / nw));
+            if (nw == 8)
+                hipLaunchKernelGGL((psa_attention_full<T, 8>), dim3((unsigned)(a.heads * B * qs)), dim3(64 * 8),
+                                   af_lds_bytes(a.T), s, a, B);
+            else
+                hipLaunchKernelGGL((psa_attention_full<T, AF_NW>), dim3((unsigned)(a.heads * B * qs)), dim3(64 * AF_NW),
+                                   af_lds_bytes(a.T), s, a, B);
             return (int)hipGetLastError();
         }
         const char* e = getenv("YH_ATTN_LDS");
