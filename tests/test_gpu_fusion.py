@@ -217,14 +217,16 @@ def test_attention_full_kernel_equals_chunked_kernel_and_pe_add(gpu, variant, dt
 @pytest.mark.parametrize("variant,dtype,batch,size", [("n", torch.bfloat16, 4, 640), ("s", torch.float16, 2, 320),
                                                       ("x", torch.bfloat16, 1, 1280), ("n", torch.float16, 2, 224)])
 def test_sppf_kernel_equals_three_maxpools(gpu, variant, dtype, batch, size):
-    """misc.hip sppf_fused (CPW 8-channel chunks of one image per workgroup: 2 by default, halved
-    until the planes fit the LDS) with 1, 2 (default), 4 and 8 chunks (YH_SPPF_CPW; 8 fits at
-    20x20, 40x40 falls back to 2) is bit-identical to three maxpool5 launches (YH_SPPF_FUSED=0).
+    """misc.hip sppf_fused (CPW 8-channel chunks of one image per workgroup: 1 or 2 by default,
+    halved until the planes fit the LDS) with the default and 1, 2, 4 and 8 chunks (YH_SPPF_CPW;
+    8 fits at 20x20, 40x40 falls back to 2) is bit-identical to three maxpool5 launches
+    (YH_SPPF_FUSED=0).
     Both switches are read at launch."""
     model = make_model(variant)
     x = synth.synth_scenes(batch, size, size, seed=35).to(gpu, dtype)
     ys = []
-    for env in ({"YH_SPPF_FUSED": "0"}, {"YH_SPPF_CPW": "1"}, {}, {"YH_SPPF_CPW": "4"}, {"YH_SPPF_CPW": "8"}):
+    for env in ({"YH_SPPF_FUSED": "0"}, {"YH_SPPF_CPW": "1"}, {}, {"YH_SPPF_CPW": "2"}, {"YH_SPPF_CPW": "4"},
+                {"YH_SPPF_CPW": "8"}):
         old = {k: os.environ.get(k) for k in ("YH_SPPF_FUSED", "YH_SPPF_CPW")}
         os.environ.update(env)
         try:

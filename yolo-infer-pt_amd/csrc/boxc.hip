@@ -341,7 +341,7 @@ __device__ __forceinline__ void bx_body(const BoxChainArgs& A, int li, char* sm)
             for (int e = 0; e < 16; ++e) d = fmaf((float)e, bx_div(v[e], sum), d);
             dist[a] = d;
         }
-        const float o0 = __shfl_xor(dist[0], 32), o1 = __shfl_xor(dist[1], 32);
+        const float o0 = xor32_swap(dist[0]), o1 = xor32_swap(dist[1]);
         const float dl = h ? o0 : dist[0], dt = h ? o1 : dist[1];
         const float dr = h ? dist[0] : o0, db = h ? dist[1] : o1;
         const int gy = h0 + oy, gx = w0 + ox;

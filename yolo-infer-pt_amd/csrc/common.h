@@ -204,6 +204,7 @@ struct BoxDflArgs {
     BoxDflLevel lv[3];
     int nlv, B, nk, nc, A;
     const void* const* io;
+    int tpw;   // 32-pixel tiles per wave: 1, 2 or 4 (wg0 offsets are computed with it)
 };
 // Fused C3k2 block with one Residual bottleneck (nets/nn.py:66-80 with n = 1 and
 // csp = False; Residual nn.py:42-49): conv1 1x1 (Cin -> 2c) -> split [a | b] ->
@@ -233,7 +234,7 @@ void csp_offsets(int ni, int nc, int no, int (&off)[9]);
 int csp_lds(int TH, int TW, int ni, int nc, int no);
 int launch_csp(int dtype, const CspArgs& a, int grid, hipStream_t s);
 
-constexpr int BOX_DFL_TPW = 4;       // 32-pixel tiles per wave (4 waves per workgroup)
+constexpr int BOX_DFL_TPW = 2;       // 32-pixel tiles per wave (4 waves per workgroup; YH_BOXDFL_TPW: 1 / 2 / 4)
 int launch_box_dfl(int dtype, const BoxDflArgs& a, hipStream_t s);
 
 // The whole box branch of the detect head (boxc.hip), one launch for all levels: box.l.0 (3x3

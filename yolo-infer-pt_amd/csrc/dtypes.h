@@ -128,6 +128,18 @@ __device__ __forceinline__ void st_chunk(gptr<T> p, const Chunk<T>& c) {
     for (int i = 0; i < (int)(sizeof(T) / 2); ++i) q[i] = __builtin_bit_cast(u32x4v, c.v[i]);
 }
 
+// lane l's x from lane l ^ 32 (the other wave half) by gfx950's v_permlane32_swap: a VALU
+// exchange, not an LDS round trip as a ds_bpermute shuffle
+__device__ __forceinline__ float xor32_swap(float x) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+    // r[0] = the low half's values in both halves, r[1] = the high half's
+    return __uint_as_float((threadIdx.x & 32) ? r[0] : r[1]);
+#else
+    return x;
+#endif
+}
+
 // XCD-aware bijective remap of a 1-D block id: blocks b and b+8 share an XCD
 // (round-robin dispatch), so give each XCD a contiguous range of logical ids.
 __device__ __forceinline__ int xcd_remap(int bid, int nwg) {

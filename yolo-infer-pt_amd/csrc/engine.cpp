@@ -1601,6 +1601,10 @@ struct Net {
         a.A = anchor_off(3, H, W);
         a.io = (const void* const*)io_dev;
         a.nk = op.bx[0].C / 16;
+        // tiles per wave (YH_BOXDFL_TPW: 1 / 2 / 4, read when the arguments are built)
+        const char* et = getenv("YH_BOXDFL_TPW");
+        a.tpw = BOX_DFL_TPW;
+        if (et && (atoi(et) == 1 || atoi(et) == 2 || atoi(et) == 4)) a.tpw = atoi(et);
         int wg = 0;
         for (int l = 0; l < 3; ++l) {
             BoxDflLevel& v = a.lv[a.nlv++];
@@ -1619,7 +1623,7 @@ struct Net {
             v.b = d.b_dev;
             v.wg0 = wg;
             const long long tiles = ((long long)B * v.H * v.W + 31) / 32;
-            wg += (int)((tiles + 4 * BOX_DFL_TPW - 1) / (4 * BOX_DFL_TPW));
+            wg += (int)((tiles + 4 * a.tpw - 1) / (4 * a.tpw));
         }
         return a;
     }

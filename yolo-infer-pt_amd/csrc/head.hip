@@ -515,13 +515,13 @@ __global__ HC_BOUNDS void head_cls(const HeadClsArgs A) {
 // 2h+1 of its pixel: the DFL softmax / expectation is lane-local, one swap across the halves
 // completes the four distances, and half h writes rows 2h, 2h+1 (32 consecutive anchors per
 // row and store instruction).
-template <typename T, int NK>
+template <typename T, int NK, int TPW>
 __device__ __forceinline__ void bd_body(const BoxDflArgs& A, int li) {
     const BoxDflLevel& V = A.lv[li];
     const int lane = threadIdx.x & 63, l32 = lane & 31, h = lane >> 5, wv = threadIdx.x >> 6;
     const int HW = V.H * V.W;
     const long long M = (long long)A.B * HW;
-    const long long tile0 = ((long long)(blockIdx.x - V.wg0) * 4 + wv) * BOX_DFL_TPW;
+    const long long tile0 = ((long long)(blockIdx.x - V.wg0) * 4 + wv) * TPW;
     if (tile0 * 32 >= M) return;
     const T* w = reinterpret_cast<const T*>(V.w);
     uint4 af[2][NK];
@@ -547,12 +547,12 @@ __device__ __forceinline__ void bd_body(const BoxDflArgs& A, int li) {
             const float4 q = *reinterpret_cast<const float4*>(V.b + 32 * h + 16 * a + i);
             bs[a][i] = q.x; bs[a][i + 1] = q.y; bs[a][i + 2] = q.z; bs[a][i + 3] = q.w;
         }
-    uint4 bf[BOX_DFL_TPW][NK];   // every tile's loads in flight at once (HBM latency)
+    uint4 bf[TPW][NK];   // every tile's loads in flight at once (HBM latency)
 #pragma unroll
-    for (int t = 0; t < BOX_DFL_TPW; ++t) load_b(tile0 + t, bf[t]);
+    for (int t = 0; t < TPW; ++t) load_b(tile0 + t, bf[t]);
     const gptr<T> yb = io_global<T>(A.io[1]);
 #pragma unroll
-    for (int t = 0; t < BOX_DFL_TPW; ++t) {
+    for (int t = 0; t < TPW; ++t) {
         const long long tt = tile0 + t;
         if (tt * 32 >= M) break;
         float dist[2];
@@ -578,7 +578,7 @@ __device__ __forceinline__ void bd_body(const BoxDflArgs& A, int li) {
             for (int i = 0; i < 16; ++i) d = fmaf((float)i, hx_div(v[i], sum), d);
             dist[a] = d;
         }
-        const float o0 = __shfl_xor(dist[0], 32), o1 = __shfl_xor(dist[1], 32);
+        const float o0 = xor32_swap(dist[0]), o1 = xor32_swap(dist[1]);
         const float dl = h ? o0 : dist[0], dt = h ? o1 : dist[1];
         const float dr = h ? dist[0] : o0, db = h ? dist[1] : o1;
         const long long m = tt * 32 + l32;
@@ -597,13 +597,13 @@ __device__ __forceinline__ void bd_body(const BoxDflArgs& A, int li) {
     }
 }
 
-template <typename T>
+template <typename T, int TPW>
 __global__ __launch_bounds__(256) void box_dfl(const BoxDflArgs A) {
     int li = 0;
     if (A.nlv > 1 && (int)blockIdx.x >= A.lv[1].wg0) li = 1;
     if (A.nlv > 2 && (int)blockIdx.x >= A.lv[2].wg0) li = 2;
-    if (A.nk == 4) bd_body<T, 4>(A, li);
-    else if (A.nk == 6) bd_body<T, 6>(A, li);
+    if (A.nk == 4) bd_body<T, 4, TPW>(A, li);
+    else if (A.nk == 6) bd_body<T, 6, TPW>(A, li);
 }
 
 }  // namespace
@@ -616,9 +616,14 @@ static int launch_box_dfl_t(const BoxDflArgs& a, hipStream_t s) {
         const BoxDflLevel& v = a.lv[l];
         if (v.wg0 != grid || v.ldx % 8 || v.wld % 8) return (int)hipErrorInvalidValue;
         const long long tiles = ((long long)a.B * v.H * v.W + 31) / 32;
-        grid += (int)((tiles + 4 * BOX_DFL_TPW - 1) / (4 * BOX_DFL_TPW));
+        grid += (int)((tiles + 4 * a.tpw - 1) / (4 * a.tpw));
     }
-    hipLaunchKernelGGL((box_dfl<T>), dim3((unsigned)grid), dim3(256), 0, s, a);
+    switch (a.tpw) {
+        case 1: hipLaunchKernelGGL((box_dfl<T, 1>), dim3((unsigned)grid), dim3(256), 0, s, a); break;
+        case 2: hipLaunchKernelGGL((box_dfl<T, 2>), dim3((unsigned)grid), dim3(256), 0, s, a); break;
+        case 4: hipLaunchKernelGGL((box_dfl<T, 4>), dim3((unsigned)grid), dim3(256), 0, s, a); break;
+        default: return (int)hipErrorInvalidValue;
+    }
     return (int)hipGetLastError();
 }
 

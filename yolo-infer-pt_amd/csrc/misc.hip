@@ -68,6 +68,7 @@ __device__ __forceinline__ void sppf_acc(float (&mx)[8], uint4 v) {
 #pragma unroll
     for (int e = 0; e < 8; ++e) mx[e] = fmaxf(mx[e], f[e]);
 }
+constexpr int SP_LB = 4;
 template <typename T>
 __global__ __launch_bounds__(256) void sppf_fused(const PoolArgs a, int cpw) {
     extern __shared__ __attribute__((aligned(16))) uint4 pln[];
@@ -78,32 +79,46 @@ __global__ __launch_bounds__(256) void sppf_fused(const PoolArgs a, int cpw) {
     uint4* p0 = pln;         // pool input / output planes (ping-pong)
     uint4* p1 = pln + NI;
     uint4* rm = pln + 2 * NI;   // row maxima
-    // item i = (pixel i / cpw, chunk i % cpw): consecutive threads, consecutive 16 B of a pixel
-    for (int i = threadIdx.x; i < NI; i += 256) {
-        const int px = i / cpw, c = i - px * cpw;
-        p0[i] = *reinterpret_cast<const uint4*>(img + (long long)px * a.ldc + 8 * c);
+    // item i = (pixel i / cpw, chunk i % cpw): consecutive threads, consecutive 16 B of a pixel;
+    // SP_LB loads in flight per thread before their LDS stores
+    for (int i0 = threadIdx.x; i0 < NI; i0 += SP_LB * 256) {
+        uint4 v[SP_LB];
+#pragma unroll
+        for (int u = 0; u < SP_LB; ++u) {
+            const int i = min(i0 + u * 256, NI - 1), px = i / cpw, c = i - px * cpw;
+            v[u] = *reinterpret_cast<const uint4*>(img + (long long)px * a.ldc + 8 * c);
+        }
+#pragma unroll
+        for (int u = 0; u < SP_LB; ++u)
+            if (i0 + u * 256 < NI) p0[i0 + u * 256] = v[u];
     }
     __syncthreads();
+    // window taps clamped into the map instead of skipped: a repeated tap leaves a max unchanged,
+    // so every item reads a fixed five
     for (int it = 0; it < 3; ++it) {
         const uint4* src = (it & 1) ? p1 : p0;
         uint4* dst = (it & 1) ? p0 : p1;
+#pragma unroll 2
         for (int i = threadIdx.x; i < NI; i += 256) {
             const int px = i / cpw, c = i - px * cpw;
             const int h = px / a.W, w = px - h * a.W;
             float mx[8];
 #pragma unroll
             for (int e = 0; e < 8; ++e) mx[e] = -INFINITY;
-            for (int wi = max(w - 2, 0); wi <= min(w + 2, a.W - 1); ++wi) sppf_acc<T>(mx, src[(h * a.W + wi) * cpw + c]);
+#pragma unroll
+            for (int d = -2; d <= 2; ++d) sppf_acc<T>(mx, src[(h * a.W + min(max(w + d, 0), a.W - 1)) * cpw + c]);
             rm[i] = f_to_chunk<T>(mx).v[0];
         }
         __syncthreads();
+#pragma unroll 2
         for (int i = threadIdx.x; i < NI; i += 256) {
             const int px = i / cpw, c = i - px * cpw;
             const int h = px / a.W, w = px - h * a.W;
             float mx[8];
 #pragma unroll
             for (int e = 0; e < 8; ++e) mx[e] = -INFINITY;
-            for (int hi = max(h - 2, 0); hi <= min(h + 2, a.H - 1); ++hi) sppf_acc<T>(mx, rm[(hi * a.W + w) * cpw + c]);
+#pragma unroll
+            for (int d = -2; d <= 2; ++d) sppf_acc<T>(mx, rm[(min(max(h + d, 0), a.H - 1) * a.W + w) * cpw + c]);
             const uint4 m = f_to_chunk<T>(mx).v[0];
             dst[i] = m;
             *reinterpret_cast<uint4*>(img + (long long)px * a.ldc + (it + 1) * a.C + 8 * c) = m;
@@ -126,11 +141,19 @@ int launch_sppf_t(const PoolArgs& a, hipStream_t s) {
                                           hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
                 attr_set = true;
             }
-            // chunks per workgroup: 2 (YH_SPPF_CPW: another count; 4 / 8 ran 47 / 86 us against
-            // 29 us for one chunk), halved until it divides the channels and
-            // the three planes fit the LDS
+            // chunks per workgroup: 1 while that gives at most 3 workgroups per CU (v11_n b32: 21.2
+            // against 22.8 us for 2; v11_x b16 1280: 81.9 against 90.4), else 2 (v11_s b64: 39.4
+            // against 57.7 us for 1; 4 / 8 ran 47 / 86 us at v11_n in round 4); YH_SPPF_CPW
+            // overrides. Halved until it divides the channels and the three planes fit the LDS.
+            static int ncu = 0;
+            if (!ncu) {
+                int dev = 0;
+                (void)hipGetDevice(&dev);
+                if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0)
+                    ncu = 256;
+            }
             const char* e = getenv("YH_SPPF_CPW");
-            int cpw = e ? std::max(1, atoi(e)) : 2;
+            int cpw = e ? std::max(1, atoi(e)) : (a.B * (a.C / 8) <= 3 * ncu ? 1 : 2);
             while (cpw > 1 && ((a.C / 8) % cpw || 3 * a.H * a.W * cpw * 16 > 160 * 1024))
                 cpw >>= 1;
             hipLaunchKernelGGL((sppf_fused<T>), dim3((unsigned)(a.B * (a.C / 8 / cpw))), dim3(256),
