@@ -23,6 +23,7 @@ namespace yh {
 namespace {
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
 
 template <typename T> struct HMfma;
 template <> struct HMfma<__bf16> {
@@ -160,26 +161,35 @@ __device__ __forceinline__ void hc_dw(const T* src, int SW, int ss, T* dst, int 
 #pragma unroll
             for (int kw = 0; kw < 3; ++kw) xv[r][kw] = *reinterpret_cast<const uint2*>(sp + ro + kw * ss);
         }
+        // the input pixels as fp32 pairs once (each feeds up to three output rows)
+        f32x2 xf[HC_RB + 2][3][2];
+#pragma unroll
+        for (int r = 0; r < HC_RB + 2; ++r)
+#pragma unroll
+            for (int kw = 0; kw < 3; ++kw) {
+                const T* xe = reinterpret_cast<const T*>(&xv[r][kw]);
+                xf[r][kw][0] = f32x2{tof(xe[0]), tof(xe[1])};
+                xf[r][kw][1] = f32x2{tof(xe[2]), tof(xe[3])};
+            }
 #pragma unroll
         for (int o = 0; o < HC_RB; ++o) {
             if (r0 + o >= DH) break;
-            float acc[4] = {0.f, 0.f, 0.f, 0.f};
+            // two channels per packed FMA (v_pk_fma_f32): each lane of it the same fused
+            // multiply-add, in the same tap order, as one fmaf per channel
+            f32x2 acc01 = f32x2{0.f, 0.f}, acc23 = f32x2{0.f, 0.f};
 #pragma unroll
             for (int kh = 0; kh < 3; ++kh)
 #pragma unroll
                 for (int kw = 0; kw < 3; ++kw) {
-                    const T* xe = reinterpret_cast<const T*>(&xv[o + kh][kw]);
                     const float4 wk = wt[kh * 3 + kw];
-                    acc[0] = fmaf(wk.x, tof(xe[0]), acc[0]);
-                    acc[1] = fmaf(wk.y, tof(xe[1]), acc[1]);
-                    acc[2] = fmaf(wk.z, tof(xe[2]), acc[2]);
-                    acc[3] = fmaf(wk.w, tof(xe[3]), acc[3]);
+                    acc01 = __builtin_elementwise_fma(f32x2{wk.x, wk.y}, xf[o + kh][kw][0], acc01);
+                    acc23 = __builtin_elementwise_fma(f32x2{wk.z, wk.w}, xf[o + kh][kw][1], acc23);
                 }
             T o4[4];
-            o4[0] = fromf<T>(silu<T>(acc[0] + bb.x));
-            o4[1] = fromf<T>(silu<T>(acc[1] + bb.y));
-            o4[2] = fromf<T>(silu<T>(acc[2] + bb.z));
-            o4[3] = fromf<T>(silu<T>(acc[3] + bb.w));
+            o4[0] = fromf<T>(silu<T>(acc01.x + bb.x));
+            o4[1] = fromf<T>(silu<T>(acc01.y + bb.y));
+            o4[2] = fromf<T>(silu<T>(acc23.x + bb.z));
+            o4[3] = fromf<T>(silu<T>(acc23.y + bb.w));
             *reinterpret_cast<uint2*>(dst + ((r0 + o) * DW + c) * ds + c0) = *reinterpret_cast<const uint2*>(o4);
         }
     }
