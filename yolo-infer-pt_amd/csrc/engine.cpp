@@ -1492,7 +1492,9 @@ struct Net {
         a.P = op.pwP;
         a.nst = (int)op.pws.size();
         a.nload = (int)op.pwl.size();
-        a.sink = op.pwLds - 1024;
+        // YH_PWC_WARM=0 (read when the arguments are built): no L2 warm-up in the prologue
+        const char* ew = getenv("YH_PWC_WARM");
+        a.sink = ew && atoi(ew) == 0 ? -1 : op.pwLds - 1024;
         a.zero = zero_dev;
         for (int z = 0; z < a.nload; ++z) {
             PwcLoad& L = a.ld[z];

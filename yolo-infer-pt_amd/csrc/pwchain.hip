@@ -149,8 +149,8 @@ __global__ __launch_bounds__(PWC_THREADS) void pw_chain(const PwChainArgs A) {
     }
     // L2 warm-up: the workgroups of one XCD (round-robin dispatch: blockIdx % 8) together touch
     // every stage's weights once, 1 KB per DMA into a scratch KB, so the stages' A-fragment loads
-    // hit L2 instead of each paying an HBM / MALL round trip
-    {
+    // hit L2 instead of each paying an HBM / MALL round trip (sink < 0: no warm-up)
+    if (A.sink >= 0) {
         const int G = (int)((gridDim.x + 7) >> 3), gi = (int)(blockIdx.x >> 3);
         const unsigned sink = lds0 + (unsigned)A.sink;
         int q0 = 0;
