@@ -44,7 +44,7 @@
 extern "C" {
 #endif
 
-#define YH_ABI_VERSION 4
+#define YH_ABI_VERSION 5
 
 /* status codes */
 #define YH_OK 0
@@ -241,11 +241,12 @@ int yh_unit_info(const yh_handle* h, int index, int batch, int height, int width
  * reproduces yh_forward's workspace and y exactly.
  *
  * yh_debug_operand copies operand `slot` (the desc's order) of op `index` out of the
- * workspace into dst as a dense (batch, H, W, C) array of the handle dtype, async on stream. */
+ * workspace into dst as a dense (batch, H, W, C) array of the handle dtype, async on stream;
+ * dst_bytes must equal that array's size at the workspace's current shape (YH_EINVAL otherwise). */
 int yh_debug_op_desc(const yh_handle* h, int index, int batch, int height, int width, char* buf, size_t size);
 int yh_debug_run_ops(yh_handle* h, const void* x, int x_u8, int batch, int height, int width, void* y, int first,
                      int last, void* stream);
-int yh_debug_operand(const yh_handle* h, int index, int slot, void* dst, void* stream);
+int yh_debug_operand(const yh_handle* h, int index, int slot, void* dst, size_t dst_bytes, void* stream);
 
 #ifdef __cplusplus
 }

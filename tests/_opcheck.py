@@ -351,9 +351,18 @@ def compare(dev, lo, hi, ref, dtype, what):
     ok = (d64 >= lo) & (d64 <= hi) & finite
     pinned = lo == hi
     ulps = (ordered(dev) - ordered(ref.to(dtype))).abs()
+    # interval width in ulps of the dtype (distinct representable values spanned - 1): how much
+    # freedom the proven bound leaves a kernel; a wide interval could hide a few-ulp error
+    width = (ordered(hi.to(dtype)) - ordered(lo.to(dtype))).abs()
+    wq = width.flatten().double()
+    if wq.numel() > 1 << 22:   # torch.quantile's size limit: a seeded sample
+        wq = wq[torch.randperm(wq.numel(), generator=torch.Generator().manual_seed(0))[:1 << 22]]
     st = dict(what=what, n=int(dev.numel()), bad=int((~ok).sum()), pinned=float(pinned.double().mean()),
               exact=float((ulps == 0).double().mean()), max_ulp=int(ulps.max()) if dev.numel() else 0,
-              over1=float((ulps > 1).double().mean()))
+              over1=float((ulps > 1).double().mean()),
+              w50=float(wq.quantile(0.5)) if wq.numel() else 0.0,
+              w99=float(wq.quantile(0.99)) if wq.numel() else 0.0,
+              wmax=int(width.max()) if dev.numel() else 0)
     if st["bad"]:
         idx = torch.nonzero(~ok)[:5].tolist()
         st["examples"] = [(tuple(i), float(d64[tuple(i)]), float(lo[tuple(i)]), float(hi[tuple(i)])) for i in idx]

@@ -12,8 +12,9 @@ is one value and the device must be bit-exact. The printed line per op gives the
 such pinned elements, the share equal to the correctly rounded exact value (oc.exact_values:
 the exact result with every error bound dropped, rounded per layer), the share more than one
 ulp from it and the largest distance in ulps (near-zero outputs of opposite sign count the
-whole range between them). Single-layer ops must also keep the share beyond one ulp under
-0.1 % (measured r05: at most 8e-5).
+whole range between them), and the interval width (p50 / p99 / max, in ulps). Single-layer
+ops must keep the share beyond one ulp under 0.1 % (measured r05: at most 8e-5) and the p99
+width at 4 ulps or less; the fused kinds have per-kind ceilings (OVER1_MAX, WIDTH99_MAX).
 
 Covered kernels (by configuration):
   * C2 v11_n bf16 640 b32 (images 0, 17, 31): the tuned conv_mx / conv_mxr / conv_rw plans incl.
@@ -21,6 +22,8 @@ Covered kernels (by configuration):
     c3k_fused in row bands and in SPLIT mode, sppf_fused, psa_attention_full, head_cls (all three
     levels, scores written straight into y), box_dfl; with YH_BOXCHAIN=1 (n bf16 b2) the opt-in
     fused box branch of the three levels (boxc.hip);
+  * C2 unfused (YH_FUSE=0 YH_PWCHAIN=0 YH_C3K=0 YH_HCLS_WIDE=0): the per-layer launches each
+    fused kernel is bit-identical to, at v11_n's shapes, under the single-layer bar;
   * v11_n fp16 640 b2: the same kernels in fp16;
   * C3 v11_s fp16 640 b64 (images 0, 63): wider conv plans, seven-launch C3k, per-layer cls
     branches (dwconv3x3_c4) and the class-rows decode (head_decode_lds);
@@ -179,6 +182,24 @@ def _check_op(d, ins, outs, x, y, H, W, nc, params, dtype):
     return st
 
 
+# Share of elements more than one ulp from the correctly rounded exact result, per op kind.
+# Single-layer ops: 0.1 % (measured r05: at most 8e-5, the cancellation elements). Fused chains
+# carry a layer's undecided roundings (1 ulp either way, both legitimate) into the next layer's
+# K-sum, and attention rounds its softmax weights to the dtype for the P.V MFMA, so those kinds
+# get a ceiling of about twice the largest share measured over C2 / n fp16 / C3 / C5 in r05
+# (gpurun_out r5final2: c3k 4.8e-2, attention 1.04e-2, pw_chain 4.9e-3, c3k2 4.1e-3, head_cls
+# 1.1e-3, stem_fused 8.6e-4, box_chain 0): a regression that stays inside the (wider) propagated
+# intervals still shows up here.
+OVER1_MAX = {"c3k": 0.10, "attention": 0.025, "pw_chain": 0.012, "c3k2": 0.01, "head_cls": 0.003,
+             "stem_fused": 0.002, "box_chain": 1e-3}
+# 99th percentile of the interval width (ulps between the lowest and highest dtype value the
+# proven bound admits) per op kind: the freedom the oracle leaves a kernel. Single-layer ops:
+# 4 ulps; the fused kinds' propagated intervals, measured r06 (tests print w50 / w99 / wmax per
+# op), get their own bound so a wide interval cannot hide a few-ulp error.
+WIDTH99_MAX = {"c3k": 16, "attention": 16, "pw_chain": 8, "c3k2": 8, "head_cls": 4, "stem_fused": 4,
+               "box_chain": 4}
+
+
 def run_op_parity(gpu, variant, dtype, batch, size, images, seed):
     from yolo_hip.engine import Engine
     model = make_model(variant)
@@ -216,15 +237,11 @@ def run_op_parity(gpu, variant, dtype, batch, size, images, seed):
             n_checked += s["n"]
             print(f"{d['label']:<28} {kernels[i] or d['kind']:<36} {s['what']:<18} n={s['n']:<9} "
                   f"pinned {s['pinned']:.5f} exact {s['exact']:.5f} >1ulp {s['over1']:.2e} max_ulp {s['max_ulp']} "
-                  f"bad {s['bad']}")
-            # every element within its proven interval. Single-layer ops besides: at most 0.1 % of
-            # the elements more than one ulp from the correctly rounded exact result (the
-            # cancellation elements, |y| << the magnitudes summed). Not asserted for the fused
-            # chains, where a layer's undecided roundings (1 ulp either way, both legitimate) feed
-            # the next layer's K-sum, nor for attention, whose softmax weights are rounded to the
-            # dtype for the P.V MFMA (r05: 2-6 % of its outputs; the interval accounts for both)
-            multi = d["kind"] in ("stem_fused", "c3k2", "c3k", "head_cls", "box_chain", "attention", "pw_chain")
-            if s["bad"] or (not multi and s["over1"] > 1e-3):
+                  f"width p50 {s['w50']:.0f} p99 {s['w99']:.0f} max {s['wmax']} bad {s['bad']}")
+            # every element within its proven interval; the share beyond one ulp and the
+            # interval width under the op kind's ceiling (OVER1_MAX, WIDTH99_MAX)
+            if (s["bad"] or s["over1"] > OVER1_MAX.get(d["kind"], 1e-3)
+                    or s["w99"] > WIDTH99_MAX.get(d["kind"], 4)):
                 failures.append((d["label"], kernels[i], s))
     assert not failures, failures[:4]
     # the stepped forward reproduces the graph forward bit for bit
@@ -235,6 +252,18 @@ def run_op_parity(gpu, variant, dtype, batch, size, images, seed):
 def test_op_parity_c2_n_bf16_b32(gpu):
     kinds, n = run_op_parity(gpu, "n", torch.bfloat16, 32, 640, (0, 17, 31), seed=21)
     assert {"stem_fused", "conv", "c3k2", "c3k", "sppf", "attention", "head_cls", "box_dfl", "pw_chain"} <= kinds, kinds
+
+
+def test_op_parity_c2_unfused(gpu, monkeypatch):
+    """C2 with every cross-layer fusion off (at handle creation): the per-layer launches that
+    each fused kernel is bit-identical to (tests/test_gpu_fusion.py) run at v11_n's fused shapes
+    and must meet the single-layer bar themselves (<= 0.1 % beyond one ulp, interval p99 width
+    <= 4 ulps), which closes the transitive pin of the fused kernels."""
+    for k in ("YH_FUSE", "YH_PWCHAIN", "YH_C3K", "YH_HCLS_WIDE"):
+        monkeypatch.setenv(k, "0")
+    kinds, n = run_op_parity(gpu, "n", torch.bfloat16, 32, 640, (0, 17, 31), seed=21)
+    assert not kinds & {"stem_fused", "c3k2", "c3k", "head_cls", "pw_chain", "box_chain"}, kinds
+    assert {"stem", "conv", "dwconv", "sppf", "attention", "decode"} <= kinds, kinds
 
 
 def test_op_parity_n_fp16(gpu):

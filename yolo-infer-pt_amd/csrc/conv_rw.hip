@@ -101,13 +101,16 @@ __device__ __forceinline__ void rw_barrier() {
     __builtin_amdgcn_s_barrier();
 }
 
-// counter mode: wait (bounded) until the LDS word at p reaches target; bump it (one lane)
-__device__ __forceinline__ void rw_spin(const unsigned* p, unsigned target) {
+// counter mode: wait (bounded) until the LDS word at p reaches target. Returns false if the
+// bound ran out: the caller then poisons its tile with NaN, so a stalled hand-off shows up as
+// wrong outputs every test catches, not as a silent race (and not as a hang or a trap)
+__device__ __forceinline__ bool rw_spin(const unsigned* p, unsigned target) {
     for (int k = 0; k < (1 << 22); ++k) {
         const unsigned v = __builtin_amdgcn_readfirstlane(*reinterpret_cast<const volatile unsigned*>(p));
-        if (v >= target) break;
+        if (v >= target) return true;
         __builtin_amdgcn_s_sleep(1);
     }
+    return false;
 }
 __device__ __forceinline__ void rw_signal(unsigned* p, int lane) {
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // this wave's LDS reads of the slot are done
@@ -477,6 +480,7 @@ __global__ __launch_bounds__(64 * NCG * NKC * NPG, (NCG * NKC * NPG >= 8 || NCG 
             for (int k = 0; k < p.pc_delay; ++k) __builtin_amdgcn_s_sleep(32);
         }
     }
+    bool stalled = false;   // counter mode: a hand-off wait ran out (rw_spin)
     for (int it = 0; it < n_it; ++it) {
         if constexpr (CM) {
             const int sl_it = it % NS;
@@ -486,12 +490,12 @@ __global__ __launch_bounds__(64 * NCG * NKC * NPG, (NCG * NKC * NPG >= 8 || NCG 
                 const int first = sl_it == NS - 1 ? NS - 1 : sl_it + NS;
                 rw_vmwait<CNTP>();
                 rw_signal(cnt + sl_it, lane);
-                rw_spin(cnt + sl_it, (unsigned)(NW * ((it - first) / NS + 1)));
+                stalled |= !rw_spin(cnt + sl_it, (unsigned)(NW * ((it - first) / NS + 1)));
             }
             if (it >= 1) {
                 // tile it + NS - 2 into the slot tile it - 2 used, once every wave is done with it
                 // (tile NS - 1, issued at it = 1, takes the ring's unused last slot)
-                if (it >= 2) rw_spin(cnt + NS + (it - 2) % NS, (unsigned)(NW * ((it - 2) / NS + 1)));
+                if (it >= 2) stalled |= !rw_spin(cnt + NS + (it - 2) % NS, (unsigned)(NW * ((it - 2) / NS + 1)));
                 issue(it + NS - 2, (it + NS - 2) % NS);
             }
         } else if (it > 0) {
@@ -539,6 +543,14 @@ __global__ __launch_bounds__(64 * NCG * NKC * NPG, (NCG * NKC * NPG >= 8 || NCG 
             }
         }
 
+        if constexpr (CM) {
+            if (stalled) {
+#pragma unroll
+                for (int j = 0; j < MB; ++j)
+#pragma unroll
+                    for (int e = 0; e < 16; ++e) acc[j][e] = __builtin_nanf("");
+            }
+        }
         if (RW_DBG(16)) continue;   // ablation: no K-chunk reduction, no epilogue
         // ---- K chunks: every chunk wave's partial tile to LDS (lane (r32, h) holds couts
         //      16 h .. 16 h + 15 of pixel r32: 4 swizzled 16-B chunks), then the shared epilogue

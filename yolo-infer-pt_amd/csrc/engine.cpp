@@ -2237,7 +2237,7 @@ struct Net {
             if (cur_plan->active[i]) launch_op((size_t)i, B, H, W, s);
     }
     // operand `slot` of op `oi` copied out of the workspace as a dense (B, h, w, C) array
-    void debug_operand(int oi, int slot, void* dst, hipStream_t s) const {
+    void debug_operand(int oi, int slot, void* dst, size_t dst_bytes, hipStream_t s) const {
         require(oi >= 0 && oi < (int)ops.size(), "op index out of range");
         const std::vector<Operand> od = operands(ops[oi]);
         require(slot >= 0 && slot < (int)od.size(), "operand slot out of range");
@@ -2245,6 +2245,11 @@ struct Net {
         const View& v = od[slot].v;
         const int lv = tensors[v.t].level;
         const size_t rows = (size_t)ws.B * (ws.H >> lv) * (ws.W >> lv);
+        // the caller sizes dst from a desc made at some (batch, H, W): a desc of another shape
+        // (or a later reserve() at a larger one) must not turn into an out-of-bounds write
+        require(dst_bytes == rows * (size_t)v.C * es, "yh_debug_operand: dst size " + std::to_string(dst_bytes) +
+                " B does not match the operand at the workspace shape (" + std::to_string(rows * (size_t)v.C * es) +
+                " B)");
         HIPCHECK(hipMemcpy2DAsync(dst, (size_t)v.C * es, ptr(v), (size_t)ldc(v) * es, (size_t)v.C * es, rows,
                                   hipMemcpyDeviceToDevice, s));
     }
@@ -2564,11 +2569,11 @@ int yh_debug_run_ops(yh_handle* h, const void* x, int x_u8, int batch, int heigh
     });
 }
 
-int yh_debug_operand(const yh_handle* h, int index, int slot, void* dst, void* stream) {
+int yh_debug_operand(const yh_handle* h, int index, int slot, void* dst, size_t dst_bytes, void* stream) {
     return guarded([&] {
         yh::require(h && dst, "null argument");
         HIPCHECK(hipSetDevice(h->net.device));
-        h->net.debug_operand(index, slot, dst, (hipStream_t)stream);
+        h->net.debug_operand(index, slot, dst, dst_bytes, (hipStream_t)stream);
     });
 }
 

@@ -16,7 +16,7 @@ if os.environ.get("YH_LIB"):
     LIB_PATH = os.environ["YH_LIB"]
 
 YH_F32, YH_F16, YH_BF16 = 0, 1, 2
-ABI_VERSION = 4
+ABI_VERSION = 5
 
 
 class YhVariant(ctypes.Structure):
@@ -66,7 +66,7 @@ _PROTOS = {
     "yh_resize_linear_host": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p]),
     "yh_debug_op_desc": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_char_p, c_size_t]),
     "yh_debug_run_ops": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_int, c_int, c_void_p]),
-    "yh_debug_operand": (c_int, [c_void_p, c_int, c_int, c_void_p, c_void_p]),
+    "yh_debug_operand": (c_int, [c_void_p, c_int, c_int, c_void_p, c_size_t, c_void_p]),
 }
 
 _lib = None

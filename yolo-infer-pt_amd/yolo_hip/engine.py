@@ -217,7 +217,7 @@ class Engine:
         o = desc["operands"][slot]
         out = torch.empty((batch, o["H"], o["W"], o["C"]), dtype=self.dtype, device=self.device)
         check(lib().yh_debug_operand(self._h, int(index), int(slot), c_void_p(out.data_ptr()),
-                                     _stream_ptr(self.device)), "debug_operand")
+                                     out.numel() * out.element_size(), _stream_ptr(self.device)), "debug_operand")
         return out
 
 

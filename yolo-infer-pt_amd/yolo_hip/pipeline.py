@@ -4,7 +4,9 @@ The reference's eval loop (main.py:264-273) runs `model(samples)` and then
 `util.non_max_suppression(outputs)` back to back for every batch. Both stay
 exactly the same computations here; only their scheduling changes:
 
-* the forward (yh_forward, a replayed HIP graph) runs on the caller's stream;
+* the forward (yh_forward, a replayed HIP graph) runs on a lane stream of its own, after an
+  event recorded on the caller's stream at submit() (so it sees everything the caller
+  queued before, e.g. the copy that filled x);
 * the NMS (yh_nms) of the same batch - and, data-parallel, the RCCL gather of
   its fixed-size results - runs on a second stream after an event;
 * the head output (B, 4+nc, A) is double-buffered: forward k+2 writes the
@@ -47,6 +49,12 @@ class DetectPipeline:
     NMS stream; submit() marks them used on the caller's stream (record_stream), so
     once the caller drops them the caching allocator does not hand their blocks to a
     later batch's NMS before the caller's queued reads have run.
+
+    The forward reads x on its lane stream, not on the caller's: nothing the caller queues
+    after submit() is ordered after it. x must not be modified in place (nor its storage
+    reused) until the returned `done` event has been waited on (wait(done), or a device
+    sync); `done` follows the batch's forward, NMS and post. x itself is record_stream'ed on
+    the lane stream, so merely dropping the last reference to it is safe.
     """
 
     def __init__(self, engine, batch, height, width, post=None, depth=2, nms_kwargs=None, nms_on_lane=False):
