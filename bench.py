@@ -357,6 +357,7 @@ def main():
     t0 = time.perf_counter()
     for _ in range(args.steps):
         last = step()
+    t_sub = time.perf_counter() - t0   # host time of the submit loop (diagnostic, stderr)
     torch.cuda.synchronize()
     if dist:
         torch.distributed.barrier()
@@ -367,6 +368,7 @@ def main():
         t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
         elapsed = t.item()
+    log(f"bench: timed region {elapsed * 1e3:.3f} ms, host submit loop {t_sub * 1e3:.3f} ms")
     dets, counts, extra = last
     kept = counts.cpu().tolist()
     gather_check = None

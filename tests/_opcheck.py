@@ -340,6 +340,14 @@ def ordered(t16):
     return torch.where(i < 0, -(i & 0x7FFF), i)
 
 
+def ulp_width(lo, hi, dtype):
+    """(hi - lo) in units of the dtype's ulp at max(|lo|, |hi|) (float64 tensor)"""
+    p, emin = (8, -126) if dtype == torch.bfloat16 else (11, -14)
+    m = torch.maximum(lo.abs(), hi.abs())
+    e = torch.floor(torch.log2(torch.where(m > 0, m, torch.ones_like(m)))).clamp(min=emin)
+    return torch.where(m > 0, (hi - lo) / torch.exp2(e - (p - 1)), torch.zeros_like(m))
+
+
 def compare(dev, lo, hi, ref, dtype, what):
     """dev (dtype tensor) within [lo, hi] everywhere; ref = the correctly rounded exact result
     (exact_values()). Returns a stats dict: elements, out-of-interval count, share of pinned
@@ -351,10 +359,12 @@ def compare(dev, lo, hi, ref, dtype, what):
     ok = (d64 >= lo) & (d64 <= hi) & finite
     pinned = lo == hi
     ulps = (ordered(dev) - ordered(ref.to(dtype))).abs()
-    # interval width in ulps of the dtype (distinct representable values spanned - 1): how much
-    # freedom the proven bound leaves a kernel; a wide interval could hide a few-ulp error
-    width = (ordered(hi.to(dtype)) - ordered(lo.to(dtype))).abs()
-    wq = width.flatten().double()
+    # interval width in ulps of the dtype at the interval's magnitude: (hi - lo) / ulp(max(|lo|, |hi|))
+    # (0: pinned, 1: two adjacent values). How much freedom the proven bound leaves a kernel: a wide
+    # interval could hide a few-ulp error. Intervals that straddle zero (the cancellation elements)
+    # measure about 2^p (p = 8 bf16, 11 fp16): their width is set by the magnitudes summed, not by |y|.
+    width = ulp_width(lo, hi, dtype)
+    wq = width.flatten()
     if wq.numel() > 1 << 22:   # torch.quantile's size limit: a seeded sample
         wq = wq[torch.randperm(wq.numel(), generator=torch.Generator().manual_seed(0))[:1 << 22]]
     st = dict(what=what, n=int(dev.numel()), bad=int((~ok).sum()), pinned=float(pinned.double().mean()),
@@ -362,7 +372,9 @@ def compare(dev, lo, hi, ref, dtype, what):
               over1=float((ulps > 1).double().mean()),
               w50=float(wq.quantile(0.5)) if wq.numel() else 0.0,
               w99=float(wq.quantile(0.99)) if wq.numel() else 0.0,
-              wmax=int(width.max()) if dev.numel() else 0)
+              w999=float(wq.quantile(0.999)) if wq.numel() else 0.0,
+              wide=float((width > 4).double().mean()) if dev.numel() else 0.0,
+              wmax=float(width.max()) if dev.numel() else 0.0)
     if st["bad"]:
         idx = torch.nonzero(~ok)[:5].tolist()
         st["examples"] = [(tuple(i), float(d64[tuple(i)]), float(lo[tuple(i)]), float(hi[tuple(i)])) for i in idx]

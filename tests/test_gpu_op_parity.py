@@ -13,8 +13,8 @@ such pinned elements, the share equal to the correctly rounded exact value (oc.e
 the exact result with every error bound dropped, rounded per layer), the share more than one
 ulp from it and the largest distance in ulps (near-zero outputs of opposite sign count the
 whole range between them), and the interval width (p50 / p99 / max, in ulps). Single-layer
-ops must keep the share beyond one ulp under 0.1 % (measured r05: at most 8e-5) and the p99
-width at 4 ulps or less; the fused kinds have per-kind ceilings (OVER1_MAX, WIDTH99_MAX).
+ops must keep the share beyond one ulp under 0.1 % (measured r05: at most 8e-5); the fused kinds
+have per-kind ceilings (OVER1_MAX), and every kind a ceiling on its interval widths (WIDTH_MAX).
 
 Covered kernels (by configuration):
   * C2 v11_n bf16 640 b32 (images 0, 17, 31): the tuned conv_mx / conv_mxr / conv_rw plans incl.
@@ -192,12 +192,20 @@ def _check_op(d, ins, outs, x, y, H, W, nc, params, dtype):
 # intervals still shows up here.
 OVER1_MAX = {"c3k": 0.10, "attention": 0.025, "pw_chain": 0.012, "c3k2": 0.01, "head_cls": 0.003,
              "stem_fused": 0.002, "box_chain": 1e-3}
-# 99th percentile of the interval width (ulps between the lowest and highest dtype value the
-# proven bound admits) per op kind: the freedom the oracle leaves a kernel. Single-layer ops:
-# 4 ulps; the fused kinds' propagated intervals, measured r06 (tests print w50 / w99 / wmax per
-# op), get their own bound so a wide interval cannot hide a few-ulp error.
-WIDTH99_MAX = {"c3k": 16, "attention": 16, "pw_chain": 8, "c3k2": 8, "head_cls": 4, "stem_fused": 4,
-               "box_chain": 4}
+# Interval width (tests/_opcheck.py ulp_width: (hi - lo) in ulps of the dtype at the interval's
+# magnitude; 0 = pinned, 1 = two adjacent values), (p50, p99) per op kind: the freedom the proven
+# bound leaves a kernel. It is the oracle's looseness, not the device's error: the (2K + 4) u
+# K-sum bound grows with K and with cancellation (|y| << sum |x w|), so the long 3x3 K-sums of C5
+# (K up to 3456) reach p99 ~1800, and fused chains carry every layer's interval into the next
+# (c3k: six layers, p50 ~1800). The device's own error is what over1 measures (share beyond one
+# ulp of the correctly rounded exact value). Bounds: ~1.5x the r06 maxima over C2 / C2 unfused /
+# n fp16 / C3 / C5 / box chain (gpurun_out r6b), so a loosened oracle shows up as well.
+# The fused kinds are pinned transitively rather than by their own intervals: each is bit-identical
+# to its per-layer launches (tests/test_gpu_fusion.py), and those launches meet the single-layer
+# bar (over1 <= 0.1 %, every element in its interval) at v11_n's shapes in test_op_parity_c2_unfused.
+WIDTH_MAX = {"conv": (128, 2700), "stem": (1, 4), "dwconv": (1, 4), "decode": (1, 2), "box_dfl": (1, 2),
+             "sppf": (0, 0), "stem_fused": (8, 360), "attention": (6, 240), "c3k2": (96, 2400),
+             "c3k": (2700, 5300), "pw_chain": (600, 4200), "head_cls": (36, 128), "box_chain": (24, 264)}
 
 
 def run_op_parity(gpu, variant, dtype, batch, size, images, seed):
@@ -237,11 +245,12 @@ def run_op_parity(gpu, variant, dtype, batch, size, images, seed):
             n_checked += s["n"]
             print(f"{d['label']:<28} {kernels[i] or d['kind']:<36} {s['what']:<18} n={s['n']:<9} "
                   f"pinned {s['pinned']:.5f} exact {s['exact']:.5f} >1ulp {s['over1']:.2e} max_ulp {s['max_ulp']} "
-                  f"width p50 {s['w50']:.0f} p99 {s['w99']:.0f} max {s['wmax']} bad {s['bad']}")
+                  f"width p50 {s['w50']:.2f} p99 {s['w99']:.2f} p99.9 {s['w999']:.1f} >4 {s['wide']:.2e} "
+                  f"max {s['wmax']:.0f} bad {s['bad']}")
             # every element within its proven interval; the share beyond one ulp and the
-            # interval width under the op kind's ceiling (OVER1_MAX, WIDTH99_MAX)
-            if (s["bad"] or s["over1"] > OVER1_MAX.get(d["kind"], 1e-3)
-                    or s["w99"] > WIDTH99_MAX.get(d["kind"], 4)):
+            # interval width under the op kind's ceilings (OVER1_MAX, WIDTH_MAX)
+            w50, w99 = WIDTH_MAX[d["kind"]]
+            if s["bad"] or s["over1"] > OVER1_MAX.get(d["kind"], 1e-3) or s["w50"] > w50 or s["w99"] > w99:
                 failures.append((d["label"], kernels[i], s))
     assert not failures, failures[:4]
     # the stepped forward reproduces the graph forward bit for bit

@@ -120,6 +120,7 @@ struct NmsArgs {
     unsigned long long* mask;   // [B][64 * 64 * 65 / 2] words
 #ifdef YH_ABLATION
     unsigned long long* trace;  // diagnostic builds only: [B][16] phase timestamps (s_memrealtime)
+    int dbg;                    // diagnostic builds only: ablation bits (YH_NMS_DBG, nms.hip)
 #endif
 };
 

@@ -2470,6 +2470,7 @@ int yh_nms(int dtype, const void* y, int batch, int num_classes, int anchors, fl
         a.max_nms = max_nms;
 #ifdef YH_ABLATION
         a.trace = nms_trace;
+        a.dbg = getenv("YH_NMS_DBG") ? atoi(getenv("YH_NMS_DBG")) : 0;
 #endif
         a.keys = (unsigned long long*)workspace;
         a.counts = (int*)((char*)workspace + (size_t)batch * anchors * num_classes * 8);

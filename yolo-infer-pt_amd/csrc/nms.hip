@@ -37,8 +37,10 @@
 // compiled out of the shipped library
 #ifdef YH_ABLATION
 #define NMS_TRACE (p.trace)
+#define NMS_DBG(bit) (p.dbg & (bit))
 #else
 #define NMS_TRACE ((unsigned long long*)nullptr)
+#define NMS_DBG(bit) 0
 #endif
 
 namespace yh {
@@ -134,6 +136,10 @@ __global__ __launch_bounds__(256) void nms_emit(const NmsArgs p) {
             if (k) rows_hit |= 0x80000000u;
         }
     }
+    if (NMS_DBG(8)) {   // ablation: loads and counts only
+        if (cnt == 12345678) p.counts[n] = 0;
+        return;
+    }
     int incl = cnt;
 #pragma unroll
     for (int d = 1; d < 64; d <<= 1) {
@@ -156,7 +162,7 @@ __global__ __launch_bounds__(256) void nms_emit(const NmsArgs p) {
                 const unsigned long long k = make_key(v[e], (unsigned)((a0 + e) * p.nc + c));
                 if (staged) lkeys[off++] = k;
                 else keys[off++] = k;
-                atomicAdd(&lhist[score_bin(v[e], p.bin_base)], 1u);
+                if (!NMS_DBG(4)) atomicAdd(&lhist[score_bin(v[e], p.bin_base)], 1u);
             }
         }
     };
@@ -177,11 +183,12 @@ __global__ __launch_bounds__(256) void nms_emit(const NmsArgs p) {
             }
     }
     __syncthreads();
-    if (staged)
+    if (staged && !NMS_DBG(2))
         for (int t = threadIdx.x; t < btot; t += 256) keys[t] = lkeys[t];
     unsigned* gh = p.hist + (long long)n * NBINS;
-    for (int i = threadIdx.x; i < NBINS; i += 256)
-        if (lhist[i]) atomicAdd(&gh[i], lhist[i]);
+    if (!NMS_DBG(1))
+        for (int i = threadIdx.x; i < NBINS; i += 256)
+            if (lhist[i]) atomicAdd(&gh[i], lhist[i]);
 }
 
 // Zeroes the per-image candidate counts, score histograms and gather counters (one

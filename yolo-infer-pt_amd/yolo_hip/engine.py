@@ -244,8 +244,16 @@ def nms_host(outputs, confidence_threshold=0.001, iou_threshold=0.65, max_det=30
     return dets, counts
 
 
-def nms(outputs, confidence_threshold=0.001, iou_threshold=0.65, max_det=300, max_nms=30000, max_wh=7680.0):
-    """On-device batched NMS of a (B, 4 + nc, A) cuda tensor -> (dets (B, max_det, 6) f32, counts (B,) i32)."""
+def nms_workspace_bytes(batch, num_classes, anchors):
+    return int(lib().yh_nms_workspace_bytes(int(batch), int(num_classes), int(anchors)))
+
+
+def nms(outputs, confidence_threshold=0.001, iou_threshold=0.65, max_det=300, max_nms=30000, max_wh=7680.0,
+        out=None, workspace=None):
+    """On-device batched NMS of a (B, 4 + nc, A) cuda tensor -> (dets (B, max_det, 6) f32, counts (B,) i32).
+
+    out=(dets, counts) and workspace (uint8, >= nms_workspace_bytes) may be given to reuse buffers
+    (yolo_hip.pipeline's result ring); otherwise they come from the caching allocator."""
     if not outputs.is_cuda:
         raise ValueError("yolo_hip.nms needs a cuda tensor")
     y = outputs.contiguous()
@@ -253,9 +261,21 @@ def nms(outputs, confidence_threshold=0.001, iou_threshold=0.65, max_det=300, ma
     nc = no - 4
     dev = y.device
     need = lib().yh_nms_workspace_bytes(B, nc, A)
-    ws = torch.empty(int(need), dtype=torch.uint8, device=dev)  # caching allocator: stream-safe reuse
-    dets = torch.empty((B, max_det, 6), dtype=torch.float32, device=dev)
-    counts = torch.empty((B,), dtype=torch.int32, device=dev)
+    if workspace is not None:
+        if workspace.dtype != torch.uint8 or workspace.numel() < need or workspace.device != dev:
+            raise ValueError(f"yolo_hip.nms: workspace must be a uint8 tensor of >= {need} bytes on {dev}")
+        ws = workspace
+    else:
+        ws = torch.empty(int(need), dtype=torch.uint8, device=dev)  # caching allocator: stream-safe reuse
+    if out is not None:
+        dets, counts = out
+        if (tuple(dets.shape) != (B, max_det, 6) or dets.dtype != torch.float32 or tuple(counts.shape) != (B,)
+                or counts.dtype != torch.int32 or dets.device != dev or counts.device != dev
+                or not dets.is_contiguous()):
+            raise ValueError("yolo_hip.nms: out must be (dets (B, max_det, 6) f32, counts (B,) i32) on the device")
+    else:
+        dets = torch.empty((B, max_det, 6), dtype=torch.float32, device=dev)
+        counts = torch.empty((B,), dtype=torch.int32, device=dev)
     with torch.cuda.device(dev):
         check(lib().yh_nms(dtype_code(y.dtype), c_void_p(y.data_ptr()), B, nc, A, ctypes.c_float(confidence_threshold),
                            c_double(iou_threshold), int(max_det), int(max_nms), ctypes.c_float(max_wh),

@@ -57,7 +57,8 @@ class DetectPipeline:
     the lane stream, so merely dropping the last reference to it is safe.
     """
 
-    def __init__(self, engine, batch, height, width, post=None, depth=2, nms_kwargs=None, nms_on_lane=False):
+    def __init__(self, engine, batch, height, width, post=None, depth=2, nms_kwargs=None, nms_on_lane=False,
+                 result_ring=False, idle_skip=True):
         # engine: one Engine, or a list of Engines with the same weights (forward lanes)
         self.engs = list(engine) if isinstance(engine, (list, tuple)) else [engine]
         self.eng = self.engs[0]
@@ -67,6 +68,17 @@ class DetectPipeline:
         self.ys = [torch.empty((batch, 4 + self.eng.num_classes, A), dtype=self.eng.dtype, device=dev)
                    for _ in range(depth)]
         self.free = [None] * depth          # NMS-done event of the batch last held by each buffer
+        # result_ring: dets / counts of slot i (and the NMS workspace) are allocated once and reused
+        # by batch k + depth; no per-batch allocation or record_stream (see submit())
+        self.result_ring = result_ring
+        if result_ring:
+            from .engine import nms_workspace_bytes
+            md = (nms_kwargs or {}).get("max_det", 300)
+            self.dets = [torch.empty((batch, md, 6), dtype=torch.float32, device=dev) for _ in range(depth)]
+            self.counts = [torch.empty((batch,), dtype=torch.int32, device=dev) for _ in range(depth)]
+            nws = len(self.engs) if nms_on_lane else 1   # one per stream the NMS runs on
+            wsb = nms_workspace_bytes(batch, self.eng.num_classes, A)
+            self.nms_ws = [torch.empty(wsb, dtype=torch.uint8, device=dev) for _ in range(nws)]
         # nms_on_lane: each batch's NMS follows its forward on the lane's stream (one
         # stream fewer: the HIP runtime maps streams onto GPU_MAX_HW_QUEUES = 4 queues)
         self.nms_stream = None if nms_on_lane else torch.cuda.Stream(device=dev)
@@ -80,6 +92,8 @@ class DetectPipeline:
             [torch.cuda.Stream(device=dev) for _ in self.engs[1:]]
         self.post = post
         self.nms_kwargs = nms_kwargs or {}
+        # idle_skip: no `ready` marker on the caller's stream when it has no pending work (see submit)
+        self.idle_skip = idle_skip
         self.k = 0
 
     def submit(self, x):
@@ -91,9 +105,15 @@ class DetectPipeline:
         fs = main
         if self.lane_streams[lane] is not None:
             fs = self.lane_streams[lane]
-            ready = torch.cuda.Event()   # x (and anything else the caller queued) is ready
-            ready.record(main)
-            fs.wait_event(ready)
+            # x (and anything else the caller queued) must be ready before the forward reads it.
+            # If the caller's stream has nothing pending, it is already: no marker is queued there.
+            # (A marker on the caller's stream sits in whatever hardware queue that stream shares
+            # with a lane - GPU_MAX_HW_QUEUES = 4 - behind that lane's queued forwards, which ties
+            # every lane's next forward to that one lane's progress.)
+            if not (self.idle_skip and main.query()):
+                ready = torch.cuda.Event()
+                ready.record(main)
+                fs.wait_event(ready)
             x.record_stream(fs)
         if self.free[i] is not None:
             fs.wait_event(self.free[i])
@@ -104,7 +124,14 @@ class DetectPipeline:
         ns = self.nms_stream if self.nms_stream is not None else fs
         with torch.cuda.stream(ns):
             ns.wait_event(fwd_done)
-            dets, counts = nms(y, **self.nms_kwargs)
+            if self.result_ring:
+                # slot i's previous results (batch k - depth) are overwritten here: this NMS runs after
+                # fwd_done, which follows `ready`, i.e. everything the caller queued before this
+                # submit() (its reads of batch k - depth included)
+                dets, counts = nms(y, out=(self.dets[i], self.counts[i]),
+                                   workspace=self.nms_ws[lane if self.nms_stream is None else 0], **self.nms_kwargs)
+            else:
+                dets, counts = nms(y, **self.nms_kwargs)
             extra = self.post(dets, counts) if self.post is not None else None
             done = torch.cuda.Event()
             done.record(ns)
@@ -112,7 +139,7 @@ class DetectPipeline:
         # allocated on the NMS stream, read on the caller's: keep the blocks out of the
         # NMS stream's free pool until the caller's work queued after `done` has run
         if ns is not main:
-            for t in (dets, counts, *_tensors(extra)):
+            for t in ((*_tensors(extra),) if self.result_ring else (dets, counts, *_tensors(extra))):
                 if t.is_cuda:
                     t.record_stream(main)
         return dets, counts, extra, done
