@@ -307,10 +307,14 @@ def main():
     if args.serial:
         args.lanes = 1
     model = build_model(args.variant)
-    eng = Engine(*model._yh_arch, dev, dtype)
-    eng.load_module(model)
     B, S = args.batch, args.size
-    eng.reserve(B, S, S)
+    engs = []
+    for _ in range(args.lanes):
+        e = Engine(*model._yh_arch, dev, dtype)
+        e.load_module(model)
+        e.reserve(B, S, S)
+        engs.append(e)
+    eng = engs[0]
     # synthetic scenes resident in HBM before timing: a ring of distinct batches per rank whose
     # total (4 x 78.6 MB at v11_n b32 640^2 bf16) exceeds the 256 MB MALL, so a step's input is
     # not left in the last-level cache by an earlier step
@@ -322,16 +326,12 @@ def main():
     gather = Gather(B, 300, dev, rank, world, slots=2 * args.lanes + 2)   # >= batches in flight
 
     post = (lambda d, c: gather(d, c)) if dist else None  # RCCL gather of the fixed-size results to rank 0
-    engs = [eng]
-    for _ in range(args.lanes - 1):
-        e = Engine(*model._yh_arch, dev, dtype)
-        e.load_module(model)
-        e.reserve(B, S, S)
-        engs.append(e)
     for e in engs:   # tune + capture each lane's graphs one at a time, before any overlap
         e.forward(x, out=y)
         torch.cuda.synchronize()
-    pipe = DetectPipeline(engs, B, S, S, post=post, nms_on_lane=args.nms_on_lane)
+    # result ring: each in-flight batch's dets / counts live in a slot allocated once (a batch's
+    # results stay valid until the caller submits 2 x lanes more batches), no per-step allocation
+    pipe = DetectPipeline(engs, B, S, S, post=post, nms_on_lane=args.nms_on_lane, result_ring=True)
 
     it = [0]
 
@@ -346,11 +346,14 @@ def main():
         # forward of this batch overlaps the NMS (+ gather) of the previous one
         return pipe.submit(xk)[:3]
 
+    # No marker kernel before the timed region: a torch fill kernel between the warm-up and the
+    # timed steps (on the null stream or the NMS stream alike) cost the 20-step region ~6 %, and
+    # 2-4 % even before the warm-up (profiles/r06_bench_marker_ab.txt). tools/trace_stats.py finds
+    # the region in a trace as the dispatches between the idle gap of the synchronize and the end
+    # marker below.
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
-    # marker dispatch for traces (tools/trace_stats.py): the timed steps follow it
-    torch.zeros(1, device=dev).fill_(7.0)
     if dist:
         torch.distributed.barrier()
     torch.cuda.synchronize()

@@ -49,9 +49,10 @@ def test_nms_workspace_bytes():
     lib = _lib.lib()
     def al(v):
         return (v + 255) // 256 * 256
-    # keys | counts | histograms | per image: state (64 B), gathered first batch (4096 keys),
-    # decoded first batch (3 x 4096 x 16 B), triangular IoU mask (64 x 64 x 65 / 2 words)
-    hist = al(2 * 8400 * 80 * 8 + 2 * 4)
+    # counts | histograms | per image: state (64 B), gathered first batch (4096 keys), decoded
+    # first batch (3 x 4096 x 16 B), triangular IoU mask (64 x 64 x 65 / 2 words); no
+    # per-candidate key list (the keys are made from the scores where needed, nms.hip)
+    hist = al(2 * 4)
     state = al(hist + 2 * 2048 * 4)
     gk = al(state + 2 * 64)
     ents = al(gk + 2 * 4096 * 8)

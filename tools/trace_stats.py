@@ -2,9 +2,10 @@
 
 python tools/trace_stats.py TRACE_DIR [steps]
 
-bench.py launches a marker fill kernel right before and right after its timed steps;
-only the dispatches between them count (the tuner's trial launches and the roofline's
-eager forwards are excluded). Prints per kernel name: calls, calls per step, total and
+bench.py launches a marker fill kernel right after its timed steps (and none before them: see
+bench.py); the timed steps are the dispatches between the last idle gap of >= 150 us before
+that marker (the synchronize + barrier between the warm-up and the timed steps) and the
+marker (the tuner's trial launches and the roofline's eager forwards are excluded). Prints per kernel name: calls, calls per step, total and
 average duration, and the busy time of the whole region (union of kernel intervals).
 """
 import csv
@@ -23,19 +24,26 @@ def main():
                 rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"]))
     rows.sort()
     marks = [i for i, r in enumerate(rows) if "fill" in r[2].lower()]
-    # a marker is torch.zeros(1) + fill_(v): consecutive fill dispatches form one cluster;
-    # the timed region lies between the last two clusters
+    # the end marker is torch.zeros(1) + fill_(8): the first fill dispatch of its cluster
     clusters = []
     for i in marks:
         if clusters and i == clusters[-1][-1] + 1:
             clusters[-1].append(i)
         else:
             clusters.append([i])
-    if len(clusters) < 2:
-        raise SystemExit("markers not found")
-    a, b = clusters[-2][-1], clusters[-1][0]
-    region = rows[a + 1:b]
-    t0, t1 = rows[a][1], rows[b][0]
+    if not clusters:
+        raise SystemExit("end marker not found")
+    b = clusters[-1][0]
+    # the region starts after the last idle gap (no kernel running) of >= 150 us before b
+    a, run_end = None, None
+    for i in range(b):
+        if run_end is not None and rows[i][0] - run_end >= 150_000:
+            a = i
+        run_end = rows[i][1] if run_end is None else max(run_end, rows[i][1])
+    if a is None:
+        raise SystemExit("no idle gap before the end marker")
+    region = rows[a:b]
+    t0, t1 = rows[a][0], rows[b][0]
     stats = {}
     for s, e, n in region:
         k = n.split("(")[0][:90]

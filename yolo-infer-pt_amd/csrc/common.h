@@ -107,8 +107,7 @@ struct NmsArgs {
     float iou;           // largest float <= iou threshold (so ovr > iou  <=>  ovr > thr)
     float max_wh;
     int max_det, max_nms;
-    unsigned long long* keys;  // [B][A*nc] candidate keys
-    int* counts;               // [B] candidate counts (zeroed by the launcher)
+    int* counts;               // [B] candidate counts (zeroed by nms_zero)
     unsigned* hist;            // [B][2048] coarse score-bin histogram (zeroed by the launcher)
     int bin_base;              // (fp32 bits >> 16) of the lowest bin
     float* dets; int* ndet;

@@ -2411,7 +2411,9 @@ int yh_forward_u8(yh_handle* h, const void* x, int batch, int height, int width,
 namespace {
 constexpr size_t NMS_STATE_B = 64, NMS_GK_B = 4096 * 8, NMS_ENTS_B = 3 * 4096 * 16, NMS_MASK_B = 64 * 64 * 65 / 2 * 8;
 size_t nms_al(size_t v) { return (v + 255) & ~(size_t)255; }
-size_t nms_off_hist(int B, int nc, int A) { return nms_al((size_t)B * A * nc * 8 + (size_t)B * 4); }
+// [counts B x i32][hist B x 2048 u32][state][gkeys][ents][mask] (no per-candidate key list: the
+// keys are made from the scores where they are needed, nms.hip for_pairs)
+size_t nms_off_hist(int B, int nc, int A) { (void)nc; (void)A; return nms_al((size_t)B * 4); }
 size_t nms_off_state(int B, int nc, int A) { return nms_al(nms_off_hist(B, nc, A) + (size_t)B * 2048 * 4); }
 size_t nms_off_gk(int B, int nc, int A) { return nms_al(nms_off_state(B, nc, A) + (size_t)B * NMS_STATE_B); }
 size_t nms_off_ents(int B, int nc, int A) { return nms_al(nms_off_gk(B, nc, A) + (size_t)B * NMS_GK_B); }
@@ -2472,8 +2474,7 @@ int yh_nms(int dtype, const void* y, int batch, int num_classes, int anchors, fl
         a.trace = nms_trace;
         a.dbg = getenv("YH_NMS_DBG") ? atoi(getenv("YH_NMS_DBG")) : 0;
 #endif
-        a.keys = (unsigned long long*)workspace;
-        a.counts = (int*)((char*)workspace + (size_t)batch * anchors * num_classes * 8);
+        a.counts = (int*)workspace;
         a.hist = (unsigned*)((char*)workspace + nms_off_hist(batch, num_classes, anchors));
         a.state = (unsigned long long*)((char*)workspace + nms_off_state(batch, num_classes, anchors));
         a.gkeys = (unsigned long long*)((char*)workspace + nms_off_gk(batch, num_classes, anchors));

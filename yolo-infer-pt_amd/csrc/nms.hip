@@ -12,13 +12,14 @@
 // there); no wall-clock cutoff (util.py:166-167 is dropped).
 //
 // Design (gfx950):
-//   nms_emit   grid (A/256, B), 8 class groups per block: every pair above conf
-//              becomes a 56-bit key (score bits << 26 | (2^26-1 - pair)); larger
-//              key = earlier in the reference order. Block-scanned, one atomic
-//              per block, plus a 2048-bin score histogram per image.
-//   nms_prep   one 1024-thread workgroup per image: the first batch of whole score
-//              bins (<= 4096 keys) gathered and bitonic-sorted in LDS, each entry
-//              decoded once into the workspace.
+//   nms_emit   grid (A/256, B), 8 class groups per block: the census of the pairs
+//              above conf: the image's count and its 2048-bin score histogram.
+//   nms_gather 8 workgroups per image: the first batch = the top whole score bins
+//              (>= FIRST_TARGET pairs, <= 4096), each pair as a 56-bit key (score bits
+//              << 26 | (2^26-1 - pair); larger key = earlier in the reference order),
+//              made from the scores (for_pairs).
+//   nms_prep   one 1024-thread workgroup per image: the first batch bitonic-sorted in
+//              LDS, each entry decoded once into the workspace.
 //   nms_mask   the first batches' lower-triangular IoU bitmasks, one wave per 64 x 64
 //              tile, the tiles of all images strided over one grid.
 //   nms_finish one workgroup per image: one wave resolves the greedy order from the
@@ -62,31 +63,45 @@ __device__ __forceinline__ unsigned long long make_key(float s, unsigned pair) {
 }
 
 constexpr int NBINS = 2048;  // coarse score bins = top 16 bits of the fp32 score, offset by the threshold's
+// Keys the first batch takes at least (whole score bins, <= CAP): the greedy of a typical image
+// reaches max_det = 300 kept within its first 400-620 keys (v11_n bf16 synthetic scenes); with
+// 640 an image continued into the single-workgroup sub-batch path in about every second batch of
+// 32 (nms_finish 10 -> 70 us). 960 still sorts as one 1024-key register bitonic (nms_prep).
+constexpr int FIRST_TARGET = 960;
 
 __device__ __forceinline__ int score_bin(float s, int base) {
     const int b = (int)(__float_as_uint(s) >> 16) - base;
     return b < 0 ? 0 : (b >= NBINS ? NBINS - 1 : b);
 }
 
-// Candidate emit: a block covers 256 anchors (32 chunks of 8 consecutive anchors,
-// one 16-B load per class row) x 8 class groups; thread (chunk, group) loads the
-// group's class rows once (the first EMIT_KEEP stay in registers), counts the passing
-// (anchor, class) pairs, and after the block scan writes their keys, staged in LDS and
-// written out contiguously (8-byte scattered stores cost more than the reads). Keys go
-// out unordered (nms_prep orders by key; the key carries the pair index).
+// Candidate census: a block covers 256 anchors (32 chunks of 8 consecutive anchors,
+// one 16-B load per class row) x 8 class groups; thread (chunk, group) loads the group's
+// class rows, counts the passing (anchor, class) pairs (util.py:147, score > conf) and adds
+// each to the block's LDS score-bin histogram; one atomic per block for the image's count,
+// one merge of the histogram. No keys are written: nms_gather makes the first batch's keys
+// from the scores again (its bins are known by then), and the rare later batches
+// (nms_rest) enumerate the pairs from the scores the same way (for_pairs). Writing every
+// candidate's 8-byte key here (up to 30 k per image) cost more than reading the scores twice.
 constexpr int EMIT_APT = 8;            // anchors per thread (one 16-B chunk)
 constexpr int EMIT_CHUNKS = 32;        // anchor chunks per block
 constexpr int EMIT_GROUPS = 8;         // class groups per block
-constexpr int EMIT_KEEP = 12;          // class rows per group held in registers (80 classes: 10)
-constexpr int EMIT_LCAP = 4096;        // keys a block stages in LDS before one coalesced write
+
+template <typename T>
+__device__ __forceinline__ void load_scores(const T* src, bool full, int n_ok, float (&v)[EMIT_APT]) {
+    if (full) {
+        chunk_to_f(ld_chunk(src), v);
+    } else {
+#pragma unroll
+        for (int e = 0; e < EMIT_APT; ++e) v[e] = e < n_ok ? tof(src[e]) : -1.0f;
+    }
+}
 
 template <typename T>
 __global__ __launch_bounds__(256) void nms_emit(const NmsArgs p) {
-    __shared__ int wtot[4];
-    __shared__ int sbase;
     __shared__ unsigned lhist[NBINS];
-    __shared__ unsigned long long lkeys[EMIT_LCAP];   // the block's keys, written out coalesced
+    __shared__ int wtot[4];
     for (int i = threadIdx.x; i < NBINS; i += 256) lhist[i] = 0;
+    __syncthreads();   // at entry: no load is in flight yet
     const int n = blockIdx.y;
     const int chunk = threadIdx.x & (EMIT_CHUNKS - 1), grp = threadIdx.x / EMIT_CHUNKS;
     const int a0 = (blockIdx.x * EMIT_CHUNKS + chunk) * EMIT_APT;
@@ -94,101 +109,66 @@ __global__ __launch_bounds__(256) void nms_emit(const NmsArgs p) {
     const int cpg = (p.nc + EMIT_GROUPS - 1) / EMIT_GROUPS;
     const int c_lo = grp * cpg, c_hi = min(p.nc, c_lo + cpg);
     const T* y = reinterpret_cast<const T*>(p.y) + (long long)n * (4 + p.nc) * p.A;
-    const bool live = a0 < p.A;
     const bool full = a0 + EMIT_APT <= p.A && (p.A % EMIT_APT) == 0;
-    auto row = [&](int c, float (&v)[EMIT_APT]) {
-        const T* src = y + (long long)(4 + c) * p.A + a0;
-        if (full) {
-            chunk_to_f(ld_chunk(src), v);
-        } else {
-#pragma unroll
-            for (int e = 0; e < EMIT_APT; ++e) v[e] = a0 + e < p.A ? tof(src[e]) : -1.0f;
-        }
-    };
-    Chunk<T> keep[EMIT_KEEP];
     int cnt = 0;
-    unsigned rows_hit = 0;   // bit i: row c_lo + i has a passing anchor; bit 31: some row past EMIT_KEEP
-    if (live) {
-        if (full) {
+    if (a0 < p.A) {
+        constexpr int U = 4;   // rows in flight per thread
+        for (int c0 = c_lo; c0 < c_hi; c0 += U) {
+            float v[U][EMIT_APT];
 #pragma unroll
-            for (int i = 0; i < EMIT_KEEP; ++i)
-                if (c_lo + i < c_hi) keep[i] = ld_chunk(y + (long long)(4 + c_lo + i) * p.A + a0);
-        }
+            for (int u = 0; u < U; ++u)
+                if (c0 + u < c_hi) load_scores(y + (long long)(4 + c0 + u) * p.A + a0, full, p.A - a0, v[u]);
 #pragma unroll
-        for (int i = 0; i < EMIT_KEEP; ++i) {
-            if (c_lo + i >= c_hi) continue;
-            float v[EMIT_APT];
-            if (full) chunk_to_f(keep[i], v);
-            else row(c_lo + i, v);
-            int k = 0;
+            for (int u = 0; u < U; ++u) {
+                if (c0 + u >= c_hi) continue;
 #pragma unroll
-            for (int e = 0; e < EMIT_APT; ++e) k += v[e] > p.conf;
-            cnt += k;
-            if (k) rows_hit |= 1u << i;
-        }
-        for (int c = c_lo + EMIT_KEEP; c < c_hi; ++c) {
-            float v[EMIT_APT];
-            row(c, v);
-            int k = 0;
-#pragma unroll
-            for (int e = 0; e < EMIT_APT; ++e) k += v[e] > p.conf;
-            cnt += k;
-            if (k) rows_hit |= 0x80000000u;
-        }
-    }
-    if (NMS_DBG(8)) {   // ablation: loads and counts only
-        if (cnt == 12345678) p.counts[n] = 0;
-        return;
-    }
-    int incl = cnt;
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-        const int v = __shfl_up(incl, d);
-        if (lane >= d) incl += v;
-    }
-    if (lane == 63) wtot[wave] = incl;
-    __syncthreads();
-    if (threadIdx.x == 0) sbase = atomicAdd(&p.counts[n], wtot[0] + wtot[1] + wtot[2] + wtot[3]);
-    __syncthreads();
-    const int btot = wtot[0] + wtot[1] + wtot[2] + wtot[3];
-    const bool staged = btot <= EMIT_LCAP;   // else (rare) each thread writes its keys directly
-    int off = incl - cnt;                     // offset within the block's keys
-    for (int w = 0; w < wave; ++w) off += wtot[w];
-    unsigned long long* keys = p.keys + (long long)n * p.A * p.nc + sbase;
-    auto put = [&](int c, const float (&v)[EMIT_APT]) {
-#pragma unroll
-        for (int e = 0; e < EMIT_APT; ++e) {
-            if (v[e] > p.conf) {
-                const unsigned long long k = make_key(v[e], (unsigned)((a0 + e) * p.nc + c));
-                if (staged) lkeys[off++] = k;
-                else keys[off++] = k;
-                if (!NMS_DBG(4)) atomicAdd(&lhist[score_bin(v[e], p.bin_base)], 1u);
+                for (int e = 0; e < EMIT_APT; ++e)
+                    if (v[u][e] > p.conf) {
+                        ++cnt;
+                        atomicAdd(&lhist[score_bin(v[u][e], p.bin_base)], 1u);
+                    }
             }
         }
-    };
-    if (cnt) {
-#pragma unroll
-        for (int i = 0; i < EMIT_KEEP; ++i) {
-            if (!((rows_hit >> i) & 1u)) continue;
-            float v[EMIT_APT];
-            if (full) chunk_to_f(keep[i], v);
-            else row(c_lo + i, v);
-            put(c_lo + i, v);
-        }
-        if (rows_hit >> 31)
-            for (int c = c_lo + EMIT_KEEP; c < c_hi; ++c) {
-                float v[EMIT_APT];
-                row(c, v);
-                put(c, v);
-            }
     }
+#pragma unroll
+    for (int d = 32; d > 0; d >>= 1) cnt += __shfl_xor(cnt, d);
+    if (lane == 0) wtot[wave] = cnt;
     __syncthreads();
-    if (staged && !NMS_DBG(2))
-        for (int t = threadIdx.x; t < btot; t += 256) keys[t] = lkeys[t];
+    if (threadIdx.x == 0) {
+        const int t = wtot[0] + wtot[1] + wtot[2] + wtot[3];
+        if (t) atomicAdd(&p.counts[n], t);
+    }
     unsigned* gh = p.hist + (long long)n * NBINS;
-    if (!NMS_DBG(1))
-        for (int i = threadIdx.x; i < NBINS; i += 256)
-            if (lhist[i]) atomicAdd(&gh[i], lhist[i]);
+    for (int i = threadIdx.x; i < NBINS; i += 256)
+        if (lhist[i]) atomicAdd(&gh[i], lhist[i]);
+}
+
+// Every candidate pair of image n (score > conf) in units [u0, u1) of one class row's 8
+// consecutive anchors (unit u = class * nq + chunk, nq = ceil(A / 8)), units strided by
+// `step` from `first`: fn(key, score) for each, in no particular order. The keys are
+// make_key's, bit for bit the ones nms_emit used to write.
+template <typename T, int U = 4, typename F>   // U: units in flight per thread
+__device__ __forceinline__ void for_pairs(const NmsArgs& p, const T* y, int u0, int u1, int first, int step, F fn) {
+    const int nq = (p.A + EMIT_APT - 1) / EMIT_APT;
+    const bool aligned = (p.A % EMIT_APT) == 0;
+    for (int ub = u0 + first; ub < u1; ub += U * step) {
+        float v[U][EMIT_APT];
+        int a0[U], c[U];
+#pragma unroll
+        for (int k = 0; k < U; ++k) {
+            const int u = ub + k * step;
+            c[k] = u / nq;
+            a0[k] = (u - c[k] * nq) * EMIT_APT;
+            if (u < u1) load_scores(y + (long long)(4 + c[k]) * p.A + a0[k], aligned, p.A - a0[k], v[k]);
+        }
+#pragma unroll
+        for (int k = 0; k < U; ++k) {
+            if (ub + k * step >= u1) continue;
+#pragma unroll
+            for (int e = 0; e < EMIT_APT; ++e)
+                if (v[k][e] > p.conf) fn(make_key(v[k][e], (unsigned)((a0[k] + e) * p.nc + c[k])));
+        }
+    }
 }
 
 // Zeroes the per-image candidate counts, score histograms and gather counters (one
@@ -578,36 +558,16 @@ __device__ void nms_batch(NmsSmem& S, const NmsArgs& p, const T* y, float* dets,
         }
 }
 
-// Append every key with pred(key) to bkeys (order irrelevant: the batch is sorted
-// next). GU loads per thread are in flight before any is consumed.
-template <typename SM, typename Pred>
-__device__ __forceinline__ void gather_keys(SM& S, const unsigned long long* keys, int nall, int tid, int lane,
-                                            Pred pred) {
-    constexpr int GU = 8;
-    for (int i0 = 0; i0 < nall; i0 += NMS_T * GU) {
-        unsigned long long k[GU];
-#pragma unroll
-        for (int u = 0; u < GU; ++u) {
-            const int i = i0 + u * NMS_T + tid;
-            k[u] = i < nall ? keys[i] : 0ull;
+// Append every candidate key of image n with pred(key) to bkeys (order irrelevant: the batch
+// is sorted next), enumerating the pairs from the scores (for_pairs) over units [u0, u1).
+template <typename T, int U = 4, typename SM, typename Pred>
+__device__ __forceinline__ void gather_pairs(SM& S, const NmsArgs& p, const T* y, int u0, int u1, int tid, Pred pred) {
+    for_pairs<T, U>(p, y, u0, u1, tid, NMS_T, [&](unsigned long long k) {
+        if (pred(k)) {
+            const int pos = atomicAdd(&S.gcount, 1);
+            if (pos < CAP) S.bkeys[pos] = k;
         }
-#pragma unroll
-        for (int u = 0; u < GU; ++u) {
-            const int i = i0 + u * NMS_T + tid;
-            const bool hit = i < nall && pred(k[u]);
-            const unsigned long long bal = __ballot(hit);
-            if (bal) {
-                const int leader = __ffsll((long long)bal) - 1;
-                int base = 0;
-                if (lane == leader) base = atomicAdd(&S.gcount, __popcll(bal));
-                base = __shfl(base, leader);
-                if (hit) {
-                    const int pos = base + __popcll(bal & ((1ull << lane) - 1ull));
-                    if (pos < CAP) S.bkeys[pos] = k[u];
-                }
-            }
-        }
-    }
+    });
 }
 
 // block-wide inclusive scan of one value per thread (1024 threads)
@@ -673,7 +633,7 @@ __device__ void bin_suffix(SM& S, const NmsArgs& p, int n, int tid, int lane, in
     __syncthreads();
 }
 
-// The first batch: whole score bins (blo, bin_hi] holding >= 640 keys (or everything left),
+// The first batch: whole score bins (blo, bin_hi] holding >= FIRST_TARGET keys (or everything left),
 // at most CAP; bcnt = 0 with flags bit 0: one bin alone exceeds CAP, bit 1: nothing to do.
 template <typename SM>
 __device__ void select_first(SM& S, int ktot, int tid, int& blo, int& bin_hi, int& bcnt, int& flags) {
@@ -684,7 +644,7 @@ __device__ void select_first(SM& S, int ktot, int tid, int& blo, int& bin_hi, in
     flags = ktot > 0 ? 0 : 2;
     while (ktot > 0) {
         const unsigned c0 = C[bin_hi + 1];
-        const unsigned target = c0 + 640u, cap = c0 + (unsigned)CAP;   // 640: typically one batch of P = 1024
+        const unsigned target = c0 + (unsigned)FIRST_TARGET, cap = c0 + (unsigned)CAP;
         if (tid == 0) {  // default: everything that is left fits the minimum batch
             S.sel_bin = -1;
             S.sel_need = (int)(C[0] - c0);
@@ -724,8 +684,9 @@ struct GatherSmem {
     unsigned wsum[NMS_T / 64];
     int sel_bin, sel_need, gcount, gbase;
 };
-constexpr int GATHER_G = 8;
+constexpr int GATHER_G = 16;   // workgroups per image (each scans 1/16 of its scores)
 
+template <typename T>
 __global__ __launch_bounds__(NMS_T) void nms_gather(const NmsArgs p) {
     __shared__ GatherSmem S;
     const int n = blockIdx.y, g = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -743,9 +704,12 @@ __global__ __launch_bounds__(NMS_T) void nms_gather(const NmsArgs p) {
         st[6] = (unsigned long long)(long long)bin_hi;
     }
     if (bcnt == 0) return;
-    const int per = (nall + gridDim.x - 1) / gridDim.x;
-    const int lo = g * per, cnt = max(0, min(nall, lo + per) - lo);
-    gather_keys(S, p.keys + (long long)n * p.A * p.nc + lo, cnt, tid, lane, [&](unsigned long long k) {
+    // this workgroup's slice of the image's (class row, 8-anchor chunk) units
+    const T* y = reinterpret_cast<const T*>(p.y) + (long long)n * (4 + p.nc) * p.A;
+    const int nu = p.nc * ((p.A + EMIT_APT - 1) / EMIT_APT);
+    const int per = (nu + gridDim.x - 1) / gridDim.x;
+    const int u0 = g * per, u1 = min(nu, u0 + per);
+    gather_pairs<T>(S, p, y, u0, u1, tid, [&](unsigned long long k) {
         const int bb = score_bin(__uint_as_float((unsigned)(k >> PBITS)), p.bin_base);
         return bb > blo && bb <= bin_hi;
     });
@@ -914,10 +878,11 @@ __global__ __launch_bounds__(MASK_T) void nms_mask(const NmsArgs p) {
 
 // The greedy over the first batch from its mask, then (rarely) the later batches.
 template <typename T>
-__device__ void nms_rest(NmsSmem& S, const NmsArgs& p, const T* y, float* dets, const unsigned long long* keys,
+__device__ void nms_rest(NmsSmem& S, const NmsArgs& p, const T* y, float* dets,
                          int nall, int ktot, int processed, unsigned long long ub, int bin_hi, bool fallback,
                          int tid, int lane, int wave) {
     const int n = blockIdx.x;
+    const int nu = p.nc * ((p.A + EMIT_APT - 1) / EMIT_APT);   // the image's (class row, chunk) units
     unsigned* C = S.hist;
     {
         const unsigned* gh = p.hist + (long long)n * NBINS;
@@ -961,7 +926,7 @@ __device__ void nms_rest(NmsSmem& S, const NmsArgs& p, const T* y, float* dets, 
         }
         if (tid == 0) S.gcount = 0;
         __syncthreads();
-        gather_keys(S, keys, nall, tid, lane, [&](unsigned long long k) {
+        gather_pairs<T, 2>(S, p, y, 0, nu, tid, [&](unsigned long long k) {
             const int bb = score_bin(__uint_as_float((unsigned)(k >> PBITS)), p.bin_base);
             return bb > blo && bb <= bin_hi;
         });
@@ -985,7 +950,7 @@ __device__ void nms_rest(NmsSmem& S, const NmsArgs& p, const T* y, float* dets, 
             __syncthreads();
             {
                 int c = 0;
-                for (int i = tid; i < nall; i += NMS_T) c += keys[i] < ub;
+                for_pairs<T, 2>(p, y, 0, nu, tid, NMS_T, [&](unsigned long long k) { c += k < ub; });
                 atomicAdd(&S.gcount, c);
             }
             __syncthreads();
@@ -1000,11 +965,10 @@ __device__ void nms_rest(NmsSmem& S, const NmsArgs& p, const T* y, float* dets, 
                     const int shift = 56 - DBITS * (lvl + 1);
                     for (int i = tid; i < HBINS; i += NMS_T) S.hist[i] = 0;
                     __syncthreads();
-                    for (int i = tid; i < nall; i += NMS_T) {
-                        const unsigned long long k = keys[i];
+                    for_pairs<T, 2>(p, y, 0, nu, tid, NMS_T, [&](unsigned long long k) {
                         if (k < ub && (lvl == 0 || (k >> (shift + DBITS)) == prefix))
                             atomicAdd(&S.hist[(k >> shift) & (HBINS - 1)], 1u);
-                    }
+                    });
                     __syncthreads();
                     constexpr int PER = HBINS / NMS_T;
                     unsigned local = 0;
@@ -1044,7 +1008,7 @@ __device__ void nms_rest(NmsSmem& S, const NmsArgs& p, const T* y, float* dets, 
             }
             if (tid == 0) S.gcount = 0;
             __syncthreads();
-            gather_keys(S, keys, nall, tid, lane, [&](unsigned long long k) { return k >= lo && k < ub; });
+            gather_pairs<T, 2>(S, p, y, 0, nu, tid, [&](unsigned long long k) { return k >= lo && k < ub; });
             __syncthreads();
             sort_batch(S, want, tid);
             nms_batch<T>(S, p, y, dets, want, tid, lane, wave);
@@ -1064,7 +1028,6 @@ __global__ __launch_bounds__(NMS_T) void nms_finish(const NmsArgs p) {
     __shared__ int nbd_s;
     const int n = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const T* y = reinterpret_cast<const T*>(p.y) + (long long)n * (4 + p.nc) * p.A;
-    const unsigned long long* keys = p.keys + (long long)n * p.A * p.nc;
     float* dets = p.dets + (long long)n * p.max_det * 6;
     const int nall = p.counts[n];
     const int ktot = min(nall, p.max_nms);
@@ -1163,7 +1126,7 @@ __global__ __launch_bounds__(NMS_T) void nms_finish(const NmsArgs p) {
     __syncthreads();
     const bool fallback = (flags & 1) != 0;
     const bool more = !(flags & 2) && want < ktot && S.kept < p.max_det && (fallback || bin_hi >= 0);
-    if (more) nms_rest<T>(S, p, y, dets, keys, nall, ktot, want, ub, bin_hi, fallback, tid, lane, wave);
+    if (more) nms_rest<T>(S, p, y, dets, nall, ktot, want, ub, bin_hi, fallback, tid, lane, wave);
     NMS_MARK(6);
     if (NMS_TRACE && tid == 0) NMS_TRACE[n * 16 + 10] = __builtin_amdgcn_s_memtime();
     if (tid == 0) p.ndet[n] = S.kept;
@@ -1182,7 +1145,7 @@ int launch_nms_t(const NmsArgs& a, hipStream_t s) {
                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)sizeof(NmsSmem));
         attr = true;
     }
-    hipLaunchKernelGGL(nms_gather, dim3(GATHER_G, a.B), dim3(NMS_T), 0, s, a);
+    hipLaunchKernelGGL((nms_gather<T>), dim3(GATHER_G, a.B), dim3(NMS_T), 0, s, a);
     hipLaunchKernelGGL((nms_prep<T>), dim3(a.B), dim3(NMS_T), sizeof(NmsSmem), s, a);
     hipLaunchKernelGGL(nms_mask, dim3(std::min(2048, 16 * a.B)), dim3(MASK_T), (a.B + 1) * sizeof(int), s, a);
     hipLaunchKernelGGL((nms_finish<T>), dim3(a.B), dim3(NMS_T), sizeof(NmsSmem), s, a);
