@@ -119,7 +119,7 @@ def roofline(eng, args, batch, prof_steps, x, y):
 
 
 PMC_SUMMARY = os.path.join(ROOT, "profiles", "pmc_traffic_latest.json")
-TRACE_PROFILE = "profiles/r04_fwd_trace_ops.txt"   # rocprofv3 per-dispatch trace of this round's library
+TRACE_PROFILE = "profiles/r06_fwd_trace_ops.txt"   # rocprofv3 per-dispatch trace of this round's library
 
 
 def pmc_traffic(cls, args):

@@ -117,6 +117,12 @@ int main(int argc, char** argv) {
         {"cls0.3 1x1 80-80 @80", 1, 1, 80, 80, 80, 80, 0, 80, 0, 0},
         {"p5.2.conv2 1x1 512-256 @20", 1, 1, 512, 256, 20, 20, 0, 512, 0, 0},
         {"h1.conv1 1x1 up256+128-128 @40", 1, 1, 384, 128, 40, 40, 0, 256, 128, 1},
+        // v11_x @1280 (C5, run with B = 16)
+        {"x p2.0 3x3s2 96-192 @320", 3, 2, 96, 192, 320, 320, 0, 96, 0, 0},
+        {"x p3.0 3x3s2 192-384 @160", 3, 2, 192, 384, 160, 160, 0, 192, 0, 0},
+        {"x p4.0 3x3s2 384-768 @80", 3, 2, 384, 768, 80, 80, 0, 384, 0, 0},
+        {"x box0.0 3x3 192-96 @160", 3, 1, 192, 96, 160, 160, 0, 192, 0, 0},
+        {"x p2.1.conv2 1x1 480-192 @320", 1, 1, 480, 192, 320, 320, 0, 480, 0, 0},
     };
     __bf16* zero;
     CK(hipMalloc(&zero, 4096));

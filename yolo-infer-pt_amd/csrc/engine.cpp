@@ -1463,6 +1463,11 @@ struct Net {
             // pick after every candidate is timed: the fastest, except that for 3x3 layers a plan
             // within 3 % of the fastest that re-reads fewer input bytes (halo and cout-slice
             // re-reads) wins - stable choices, less HBM pressure beside the other lanes
+            // YH_TUNE_CU=1 (experiment): rank by CU-time (time x CUs the grid occupies) instead of
+            // time: with lanes overlapping, a plan that leaves CUs to the other lanes can win
+            if (getenv("YH_TUNE_CU"))
+                for (size_t c = 0; c < cands[i].size(); ++c)
+                    t_ms[c] *= (float)std::min(cands[i][c].grid, num_cus) / (float)num_cus;
             const float best = *std::min_element(t_ms.begin(), t_ms.end());
             size_t pick = 0;
             for (size_t c = 0; c < cands[i].size(); ++c) {

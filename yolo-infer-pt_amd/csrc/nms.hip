@@ -112,7 +112,7 @@ __global__ __launch_bounds__(256) void nms_emit(const NmsArgs p) {
     const bool full = a0 + EMIT_APT <= p.A && (p.A % EMIT_APT) == 0;
     int cnt = 0;
     if (a0 < p.A) {
-        constexpr int U = 4;   // rows in flight per thread
+        constexpr int U = 5;   // rows in flight per thread (55 VGPRs: 8 waves per SIMD)
         for (int c0 = c_lo; c0 < c_hi; c0 += U) {
             float v[U][EMIT_APT];
 #pragma unroll
@@ -1147,7 +1147,8 @@ int launch_nms_t(const NmsArgs& a, hipStream_t s) {
     }
     hipLaunchKernelGGL((nms_gather<T>), dim3(GATHER_G, a.B), dim3(NMS_T), 0, s, a);
     hipLaunchKernelGGL((nms_prep<T>), dim3(a.B), dim3(NMS_T), sizeof(NmsSmem), s, a);
-    hipLaunchKernelGGL(nms_mask, dim3(std::min(2048, 16 * a.B)), dim3(MASK_T), (a.B + 1) * sizeof(int), s, a);
+    // about one 64 x 64 tile per wave at the typical first batch (~1000 entries: 136 tiles per image)
+    hipLaunchKernelGGL(nms_mask, dim3(std::min(4096, 32 * a.B)), dim3(MASK_T), (a.B + 1) * sizeof(int), s, a);
     hipLaunchKernelGGL((nms_finish<T>), dim3(a.B), dim3(NMS_T), sizeof(NmsSmem), s, a);
     return (int)hipGetLastError();
 }

@@ -81,6 +81,7 @@ class DetectPipeline:
             self.nms_ws = [torch.empty(wsb, dtype=torch.uint8, device=dev) for _ in range(nws)]
         # nms_on_lane: each batch's NMS follows its forward on the lane's stream (one
         # stream fewer: the HIP runtime maps streams onto GPU_MAX_HW_QUEUES = 4 queues)
+        # (stream priorities were measured in r06: a high-priority NMS stream or lane cost 1-6 %)
         self.nms_stream = None if nms_on_lane else torch.cuda.Stream(device=dev)
         # every lane on a stream of its own: the caller's stream then holds only the caller's
         # work, so the event a lane waits on before reading x (recorded there at submit) does
