@@ -96,9 +96,11 @@ def roofline(eng, args, batch, prof_steps, x, y):
                 kernel=("dense 3x3 convs: conv_mx (staged weights) / conv_mxr (resident weights) implicit GEMM "
                         "on v_mfma_f32_32x32x16, LDS-DMA patch staging, plan autotuned per layer")
                 if args.dtype != "fp32" else "dense 3x3 convs: conv_gemm (fp32 FMA implicit GEMM)",
-                timing="HIP events around each launch on the forward's stream, eager (one forward at a time); "
-                       f"{TRACE_PROFILE} holds the rocprofv3 per-dispatch trace of the same "
-                       "forwards replayed as graphs (tools/fwd_trace.py + tools/trace_ops.py)",
+                timing="HIP events around each launch on the forward's stream, eager (one forward at a time), "
+                       "the launches enqueued behind a hold kernel so they run back to back as in the replayed "
+                       f"graph (no host launch gaps inside the events); {TRACE_PROFILE} holds the rocprofv3 "
+                       "per-dispatch trace of the same forwards replayed as graphs (tools/fwd_trace.py + "
+                       "tools/trace_ops.py)",
                 launches_per_step=dom["launches"],
                 avg_launch_us=round(dom["ms"] * 1e3 / dom["launches"], 2),
                 algorithmic_bytes_per_launch=round(dom["bytes"] / dom["launches"]),

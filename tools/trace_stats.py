@@ -3,9 +3,9 @@
 python tools/trace_stats.py TRACE_DIR [steps]
 
 bench.py launches a marker fill kernel right after its timed steps (and none before them: see
-bench.py); the timed steps are the dispatches between the last idle gap of >= 150 us before
-that marker (the synchronize + barrier between the warm-up and the timed steps) and the
-marker (the tuner's trial launches and the roofline's eager forwards are excluded). Prints per kernel name: calls, calls per step, total and
+bench.py); the timed steps are the dispatches from the `steps`-th last forward's first
+dispatch (set_io) before that marker up to the marker (the tuner's trial launches, the
+warm-up steps and the roofline's eager forwards are excluded). Prints per kernel name: calls, calls per step, total and
 average duration, and the busy time of the whole region (union of kernel intervals).
 """
 import csv
@@ -34,14 +34,12 @@ def main():
     if not clusters:
         raise SystemExit("end marker not found")
     b = clusters[-1][0]
-    # the region starts after the last idle gap (no kernel running) of >= 150 us before b
-    a, run_end = None, None
-    for i in range(b):
-        if run_end is not None and rows[i][0] - run_end >= 150_000:
-            a = i
-        run_end = rows[i][1] if run_end is None else max(run_end, rows[i][1])
-    if a is None:
-        raise SystemExit("no idle gap before the end marker")
+    # every forward starts with one set_io dispatch: the region starts at the `steps`-th last
+    # set_io before b (the earlier ones are the warm-up steps')
+    sio = [i for i in range(b) if "set_io" in rows[i][2]]
+    if len(sio) < steps:
+        raise SystemExit(f"only {len(sio)} forwards before the end marker")
+    a = sio[-steps]
     region = rows[a:b]
     t0, t1 = rows[a][0], rows[b][0]
     stats = {}
