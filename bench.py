@@ -96,11 +96,9 @@ def roofline(eng, args, batch, prof_steps, x, y):
                 kernel=("dense 3x3 convs: conv_mx (staged weights) / conv_mxr (resident weights) implicit GEMM "
                         "on v_mfma_f32_32x32x16, LDS-DMA patch staging, plan autotuned per layer")
                 if args.dtype != "fp32" else "dense 3x3 convs: conv_gemm (fp32 FMA implicit GEMM)",
-                timing="HIP events around each launch on the forward's stream, eager (one forward at a time), "
-                       "the launches enqueued behind a hold kernel so they run back to back as in the replayed "
-                       f"graph (no host launch gaps inside the events); {TRACE_PROFILE} holds the rocprofv3 "
-                       "per-dispatch trace of the same forwards replayed as graphs (tools/fwd_trace.py + "
-                       "tools/trace_ops.py)",
+                timing="HIP events around each launch on the forward's stream, eager (one forward at a time); "
+                       f"{TRACE_PROFILE} holds the rocprofv3 per-dispatch trace of the same "
+                       "forwards replayed as graphs (tools/fwd_trace.py + tools/trace_ops.py)",
                 launches_per_step=dom["launches"],
                 avg_launch_us=round(dom["ms"] * 1e3 / dom["launches"], 2),
                 algorithmic_bytes_per_launch=round(dom["bytes"] / dom["launches"]),
@@ -298,6 +296,10 @@ def main():
     if dist:
         torch.cuda.set_device(local)
         torch.distributed.init_process_group("nccl", device_id=torch.device("cuda", local))
+        # the barriers around the timed steps on a CPU (gloo) group: an RCCL barrier launches a
+        # kernel, and a foreign kernel right before the timed steps slows the following milliseconds
+        # of ours (profiles/r06_bench_marker_ab.txt); the results' gather stays on RCCL
+        bar_group = torch.distributed.new_group(backend="gloo")
     dev = torch.device("cuda", local)
     dtype = DTYPES[args.dtype]
 
@@ -357,7 +359,7 @@ def main():
         step()
     torch.cuda.synchronize()
     if dist:
-        torch.distributed.barrier()
+        torch.distributed.barrier(group=bar_group)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
@@ -365,7 +367,7 @@ def main():
     t_sub = time.perf_counter() - t0   # host time of the submit loop (diagnostic, stderr)
     torch.cuda.synchronize()
     if dist:
-        torch.distributed.barrier()
+        torch.distributed.barrier(group=bar_group)
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     torch.zeros(1, device=dev).fill_(8.0)   # end marker (outside the timed region)

@@ -307,7 +307,6 @@ int launch_sppf(int dtype, const PoolArgs& a, hipStream_t s);
 int launch_attention(int dtype, const AttnArgs& a, int B, hipStream_t s);
 int launch_decode(int dtype, const DecodeArgs& a, hipStream_t s);
 int launch_set_io(void** io, const void* x, void* y, hipStream_t s);
-int launch_hold(int us, hipStream_t s);
 int launch_nms(int dtype, const NmsArgs& a, hipStream_t s);
 
 }  // namespace yh

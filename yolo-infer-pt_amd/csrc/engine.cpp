@@ -1851,10 +1851,6 @@ struct Net {
                 prof_calls.assign(nu, 0);
                 prof_key = GraphKey{B, H, W};
             }
-            // the launches are enqueued behind a hold on the stream (longer than enqueueing them
-            // takes), so they run back to back as in the replayed graph: the events time the kernels,
-            // not the host's launch gaps (eager launches of short kernels otherwise starve the GPU)
-            require(launch_hold(40 * (int)nu, s) == 0, "hold launch failed", YH_EHIP);
             for (size_t i = 0; i < nu; ++i) {
                 HIPCHECK(hipEventRecord(ev[2 * i], s));
                 launch_unit(cur_plan->units[i], B, H, W, s);

@@ -1026,20 +1026,6 @@ int launch_decode(int dtype, const DecodeArgs& a, hipStream_t s) {
     return (int)hipErrorInvalidValue;
 }
 
-// Holds the stream for `us` microseconds (one wave, s_sleep against the 100 MHz constant clock;
-// always ends). Profile mode only (Net::forward with yh_profile on): the host enqueues the eager
-// forward's launches and their timing events behind it, so the GPU then runs them back to back
-// as in the replayed graph, and the per-launch event times measure kernels, not host launch gaps.
-__global__ void hold_stream(unsigned long long ticks) {
-    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
-    while (__builtin_amdgcn_s_memrealtime() - t0 < ticks) __builtin_amdgcn_s_sleep(127);
-}
-
-int launch_hold(int us, hipStream_t s) {
-    hipLaunchKernelGGL(hold_stream, dim3(1), dim3(64), 0, s, (unsigned long long)us * 100ull);
-    return (int)hipGetLastError();
-}
-
 int launch_set_io(void** io, const void* x, void* y, hipStream_t s) {
     hipLaunchKernelGGL(set_io, dim3(1), dim3(1), 0, s, io, x, y);
     return (int)hipGetLastError();
