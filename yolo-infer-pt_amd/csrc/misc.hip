@@ -70,10 +70,13 @@ __device__ __forceinline__ void sppf_acc(float (&mx)[8], uint4 v) {
 }
 constexpr int SP_LB = 4;
 template <typename T>
-__global__ __launch_bounds__(256) void sppf_fused(const PoolArgs a, int cpw) {
+__global__ __launch_bounds__(256) void sppf_fused(const PoolArgs a, int cpw, int xcd) {
     extern __shared__ __attribute__((aligned(16))) uint4 pln[];
     const int cpp = a.C / 8, ng = cpp / cpw;
-    const int n = blockIdx.x / ng, cc = (blockIdx.x - n * ng) * cpw;
+    // xcd: an image's chunk workgroups on one XCD (consecutive logical ids), so the four 16-B
+    // chunks of a 64-B segment are fetched into one L2 instead of four
+    const int L = xcd ? xcd_remap(blockIdx.x, gridDim.x) : (int)blockIdx.x;
+    const int n = L / ng, cc = (L - n * ng) * cpw;
     const int HW = a.H * a.W, NI = HW * cpw;
     T* img = reinterpret_cast<T*>(a.buf) + (long long)n * HW * a.ldc + cc * 8;
     uint4* p0 = pln;         // pool input / output planes (ping-pong)
@@ -156,8 +159,12 @@ int launch_sppf_t(const PoolArgs& a, hipStream_t s) {
             int cpw = e ? std::max(1, atoi(e)) : (a.B * (a.C / 8) <= 3 * ncu ? 1 : 2);
             while (cpw > 1 && ((a.C / 8) % cpw || 3 * a.H * a.W * cpw * 16 > 160 * 1024))
                 cpw >>= 1;
+            // an image's chunk workgroups on one XCD (YH_SPPF_XCD=0: hardware order). r06, v11_n b32:
+            // 20.4 -> 16.3 us, PMC traffic 2.34x -> 0.67x algorithmic; v11_x b16 1280: 83 -> 56 us
+            const char* ex = getenv("YH_SPPF_XCD");
+            const int xcd = ex ? atoi(ex) : 1;
             hipLaunchKernelGGL((sppf_fused<T>), dim3((unsigned)(a.B * (a.C / 8 / cpw))), dim3(256),
-                               3 * a.H * a.W * cpw * (int)sizeof(uint4), s, a, cpw);
+                               3 * a.H * a.W * cpw * (int)sizeof(uint4), s, a, cpw, xcd);
             return (int)hipGetLastError();
         }
     }
