@@ -275,7 +275,8 @@ struct PwcRun {
 struct PwcStage {
     int K, N, act, nrun;
     PwcRun run[PWC_MAX_RUNS];
-    const void* w; int wld;            // row-major [>= N][wld] 16-bit weights (conv's w_dev, ld Kp)
+    const void* w; int wld;            // 16-bit weights in A-fragment order: fragment (a, kb) = 1 KB at
+                                       // (a * (wld / 16) + kb) KB, lane-major (engine upload "pwfrag")
     const float* bias;                 // >= N floats
     int res_lds, res_ldl;              // residual in LDS (byte offset of channel 0, stride) or -1; a
                                        // residual no stage of the chain writes comes by the prologue

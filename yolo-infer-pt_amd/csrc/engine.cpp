@@ -1154,6 +1154,22 @@ struct Net {
                             wp[(size_t)o * d.Kp + kk] = d.wf[o * per + (size_t)cl * d.k * d.k + kh * d.k + kw];
                     }
             d.w_dev = to_device(wp);
+            if (d.k == 1 && dtype != F32 && d.Kp % 16 == 0) {
+                // the same 16-bit weights in MFMA A-fragment order for pw_chain: fragment (a, kb) =
+                // couts 32a .. 32a + 31 x k 16kb .. 16kb + 15 as 64 lanes x 16 B (lane l: cout 32a +
+                // (l & 31), k 16kb + 8 (l >> 5) .. + 7), one contiguous KB, so a wave's fragment load
+                // is one coalesced KB instead of 32 strided rows
+                const int na = (d.cout + 31) / 32, nkb = d.Kp / 16;
+                std::vector<float> fr((size_t)na * 32 * d.Kp, 0.0f);
+                for (int a = 0; a < na; ++a)
+                    for (int kb = 0; kb < nkb; ++kb)
+                        for (int l = 0; l < 64; ++l)
+                            for (int e = 0; e < 8; ++e) {
+                                const int o = a * 32 + (l & 31), k = kb * 16 + 8 * (l >> 5) + e;
+                                fr[(((size_t)a * nkb + kb) * 64 + l) * 8 + e] = o < d.coutp_pad ? wp[(size_t)o * d.Kp + k] : 0.0f;
+                            }
+                d.mx_w["pwfrag"] = to_device(fr);
+            }
             HIPCHECK(hipMalloc(&d.ktab_dev, ktab.size() * 4));
             HIPCHECK(hipMemcpy(d.ktab_dev, ktab.data(), ktab.size() * 4, hipMemcpyHostToDevice));
         } else if (d.kind == CK_FIRST) {
@@ -1530,7 +1546,10 @@ struct Net {
                     R.ld = op.pwl[pr.load].C + 8;
                 }
             }
-            st.w = d.w_dev;
+            // A-fragment-ordered copy (upload: "pwfrag"); wld = Kp gives its k-blocks per A tile
+            auto itw = d.mx_w.find("pwfrag");
+            require(itw != d.mx_w.end(), "pw_chain: no fragment-ordered weights for " + d.name);
+            st.w = itw->second;
             st.wld = d.Kp;
             st.bias = d.b_dev;
             st.res_lds = -1;

@@ -9,8 +9,8 @@
 //   prologue  every global input and residual of the chain (views no earlier stage writes) ->
 //             LDS by LDS-DMA, padded by one 16-B chunk per pixel;
 //   stage     (32-cout A tile, 32-pixel B tiles) units over the waves; A fragments come from the
-//             conv's row-major 16-bit weights (L2, warmed by the prologue), 8 K blocks per piece
-//             with the next piece in flight; B fragments from LDS; epilogue: bias, activation,
+//             conv's 16-bit weights in fragment order (one contiguous KB per load; L2, warmed by
+//             the prologue), 8 K blocks per piece with the next piece in flight; B fragments from LDS; epilogue: bias, activation,
 //             one rounding, the residual (LDS) added in fp32 and rounded again; every output goes to its
 //             global view (all tensors stay materialised as in the per-layer forward) and, when a
 //             later stage reads it, to an LDS region of its own.
@@ -99,12 +99,13 @@ __global__ __launch_bounds__(PWC_THREADS) void pw_chain(const PwChainArgs A) {
     auto nsplit_of = [&](int s) { return ((A.st[s].N >> 5) >= PNW || nb < 2) ? 1 : 2; };
     auto nu_of = [&](int s) { return (A.st[s].N >> 5) * nsplit_of(s); };
     // A fragments of one step (stage s, unit u, piece pc: 8 K blocks of the unit's 32 couts)
+    // (fragment-ordered weights: each of the 8 loads is one contiguous KB of the wave)
     auto load_a = [&](int s, int u, int pc, uint4 (&f)[8]) {
         const PwcStage& S = A.st[s];
         const int a = nsplit_of(s) == 1 ? u : (u >> 1);
-        const T* wrow = reinterpret_cast<const T*>(S.w) + (long long)(a * 32 + l32) * S.wld + 8 * h + pc * 128;
+        const char* wb = reinterpret_cast<const char*>(S.w) + (((long long)a * (S.wld >> 4) + pc * 8) * 64 + lane) * 16;
 #pragma unroll
-        for (int i = 0; i < 8; ++i) f[i] = *reinterpret_cast<const uint4*>(wrow + i * 16);
+        for (int i = 0; i < 8; ++i) f[i] = *reinterpret_cast<const uint4*>(wb + i * 1024);
     };
     // the wave's steps in order - stages, its units, their pieces - with the next step's A
     // fragments in flight during the current one, across unit and stage boundaries (a stage's
