@@ -148,4 +148,34 @@ __device__ __forceinline__ int xcd_remap(int bid, int nwg) {
     return base + (bid >> 3);
 }
 
+// Touch every 64-B line of a kernel's argument block (the first `bytes` <= 1 KB of the kernarg
+// segment) with 16 scalar loads issued back to back and one wait, so the kernel's later argument
+// reads hit the scalar cache: a large argument struct read with data-dependent indices otherwise
+// pays one L2 round trip per line, one after another (pw_chain's prologue: ~4 us of such chains).
+// One asm block: the compiler's own scheduling split the loads over three waits.
+template <int bytes>
+__device__ __forceinline__ void touch_kernargs() {
+    static_assert(bytes > 0 && bytes <= 1024, "touch_kernargs: at most 16 lines");
+#if defined(__HIP_DEVICE_COMPILE__)
+    constexpr int last = ((bytes - 1) / 64) * 64;
+#define YH_KL(i) ((i) * 64 < last ? (i) * 64 : last)
+    unsigned r[16];
+    asm volatile(
+        "s_load_dword %0, %16, %17\n\ts_load_dword %1, %16, %18\n\ts_load_dword %2, %16, %19\n\t"
+        "s_load_dword %3, %16, %20\n\ts_load_dword %4, %16, %21\n\ts_load_dword %5, %16, %22\n\t"
+        "s_load_dword %6, %16, %23\n\ts_load_dword %7, %16, %24\n\ts_load_dword %8, %16, %25\n\t"
+        "s_load_dword %9, %16, %26\n\ts_load_dword %10, %16, %27\n\ts_load_dword %11, %16, %28\n\t"
+        "s_load_dword %12, %16, %29\n\ts_load_dword %13, %16, %30\n\ts_load_dword %14, %16, %31\n\t"
+        "s_load_dword %15, %16, %32\n\ts_waitcnt lgkmcnt(0)"
+        : "=&s"(r[0]), "=&s"(r[1]), "=&s"(r[2]), "=&s"(r[3]), "=&s"(r[4]), "=&s"(r[5]), "=&s"(r[6]), "=&s"(r[7]),
+          "=&s"(r[8]), "=&s"(r[9]), "=&s"(r[10]), "=&s"(r[11]), "=&s"(r[12]), "=&s"(r[13]), "=&s"(r[14]),
+          "=&s"(r[15])
+        : "s"(__builtin_amdgcn_kernarg_segment_ptr()), "n"(YH_KL(0)), "n"(YH_KL(1)), "n"(YH_KL(2)), "n"(YH_KL(3)),
+          "n"(YH_KL(4)), "n"(YH_KL(5)), "n"(YH_KL(6)), "n"(YH_KL(7)), "n"(YH_KL(8)), "n"(YH_KL(9)), "n"(YH_KL(10)),
+          "n"(YH_KL(11)), "n"(YH_KL(12)), "n"(YH_KL(13)), "n"(YH_KL(14)), "n"(YH_KL(15))
+        : "memory");
+#undef YH_KL
+#endif
+}
+
 }  // namespace yh

@@ -85,6 +85,9 @@ template <typename T>
 __global__ __launch_bounds__(PWC_THREADS) void pw_chain(const PwChainArgs A) {
     PWC_STAMP(0, true);
     PWC_STAMP(30, false);
+#ifndef YH_PWC_NOTOUCH
+    touch_kernargs<sizeof(PwChainArgs)>();
+#endif
     extern __shared__ __attribute__((aligned(16))) char sm[];
     typedef __attribute__((address_space(3))) char* lds_c;
     const unsigned lds0 = (unsigned)(size_t)(lds_c)sm;
@@ -133,9 +136,13 @@ __global__ __launch_bounds__(PWC_THREADS) void pw_chain(const PwChainArgs A) {
     advance();
     if (ps < A.nst) load_a(ps, pu, ppc, ring[1]);
     int kstep = 0;
+    PWC_STAMP(24, false);
 
     // prologue: the chain's global inputs -> LDS (pixel p, chunk c at (p * (nchunk + 1) + c) * 16;
     // the pad chunk and pixels past the map read zeros)
+#if defined(YH_PWC_TRACE) && defined(YH_PWC_NOIN)
+    if (A.nload < 0)
+#endif
     for (int g = 0; g < A.nload; ++g) {
         const PwcLoad& L = A.ld[g];
         const int cpx = L.nchunk + 1, total = A.P * cpx;
@@ -148,6 +155,7 @@ __global__ __launch_bounds__(PWC_THREADS) void pw_chain(const PwChainArgs A) {
             pc_glds(src, lds0 + (unsigned)L.lds + (unsigned)i0 * 16);
         }
     }
+    PWC_STAMP(25, false);
     // L2 warm-up: the workgroups of one XCD (round-robin dispatch: blockIdx % 8) together touch
     // every stage's weights once, 1 KB per DMA into a scratch KB, so the stages' A-fragment loads
     // hit L2 instead of each paying an HBM / MALL round trip (sink < 0: no warm-up)
@@ -162,7 +170,9 @@ __global__ __launch_bounds__(PWC_THREADS) void pw_chain(const PwChainArgs A) {
             q0 += nq;
         }
     }
+    PWC_STAMP(26, false);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    PWC_STAMP(27, false);
     pc_barrier();
     PWC_STAMP(1, false);
 
