@@ -117,6 +117,16 @@ __device__ __forceinline__ void rw_signal(unsigned* p, int lane) {
     if (lane == 0) __hip_atomic_fetch_add(p, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 
+// LDS column of patch column pcol (and back): stride 2 stores a row's even columns first
+template <int S, int PC>
+__host__ __device__ constexpr int rw_lcol(int pcol) {
+    return S == 2 ? ((pcol & 1) ? (PC + 1) / 2 + (pcol >> 1) : (pcol >> 1)) : pcol;
+}
+template <int S, int PC>
+__host__ __device__ constexpr int rw_gcol(int lcol) {
+    return S == 2 ? (lcol < (PC + 1) / 2 ? 2 * lcol : 2 * (lcol - (PC + 1) / 2) + 1) : lcol;
+}
+
 __device__ __forceinline__ uint32_t rw_fdiv(uint32_t x, FastDiv d) {
     return (uint32_t)(((uint64_t)__umulhi(x, d.m) + x) >> d.s);
 }
@@ -213,14 +223,18 @@ __global__ __launch_bounds__(64 * NCG * NKC * NPG, (NCG * NKC * NPG >= 8 || NCG 
     auto swz = [&](int prow, int pcol) { return ((pcol >> sw_sh) + prow * sw_mr) & (CPP - 1); };
 
     // ---- patch fill slots of this lane (tile independent): packed prow | pcol << 8, and
-    //      the byte offset of the source chunk from the tile's tap-(0,0) pixel
+    //      the byte offset of the source chunk from the tile's tap-(0,0) pixel. A stride-2 patch
+    //      row is stored de-interleaved (its even columns, then its odd ones: rw_lcol), so a tap's
+    //      32 B-fragment pixels are consecutive in LDS as at stride 1; otherwise every 16-lane
+    //      group of a ds_read_b128 hit 8 of the 16 bank slots (2-way conflicts on every read)
     int fgeo[NBI], foff[NBI];
 #pragma unroll
     for (int i = 0; i < NBI; ++i) {
         const int q = (i * NW + wv) * 64 + lane;
         const int ppix = q / CPP, cs = q & (CPP - 1);
-        const int prow = ppix / PC, pcol = ppix - prow * PC;
-        const int c = cs ^ swz(prow, pcol);
+        const int prow = ppix / PC, lcol = ppix - prow * PC;
+        const int pcol = rw_gcol<S, PC>(lcol);
+        const int c = cs ^ swz(prow, lcol);
         fgeo[i] = ppix < PR * PC ? (prow | (pcol << 8)) : -1;
         foff[i] = (prow * p.Wi + pcol) * p.ldc0 * 2 + c * 16;
     }
@@ -236,7 +250,8 @@ __global__ __launch_bounds__(64 * NCG * NKC * NPG, (NCG * NKC * NPG >= 8 || NCG 
             const int prow = S * pty[j] + t / 3, pcol = S * ptx[j] + t % 3;
             // the wave's K chunk starts at block kc * CBC: its chunk bits are folded in here,
             // so the k-step loop XORs compile-time block offsets only
-            bidx[t][j] = ((prow * PC + pcol) * CPP + (h ^ swz(prow, pcol))) ^ (2 * kc * CBC);
+            const int lcol = rw_lcol<S, PC>(pcol);
+            bidx[t][j] = ((prow * PC + lcol) * CPP + (h ^ swz(prow, lcol))) ^ (2 * kc * CBC);
         }
     }
 
@@ -588,7 +603,7 @@ __global__ __launch_bounds__(64 * NCG * NKC * NPG, (NCG * NKC * NPG >= 8 || NCG 
 namespace {
 
 // extra LDS cycles of the B-fragment reads of one wave over a whole tile (ds_read_b128
-// lane groups, 16-B slots of a 256-B bank row), for swizzle f = ((pcol >> sh) + prow mr) & (cpp-1)
+// lane groups, 16-B slots of a 256-B bank row), for swizzle f = ((lcol >> sh) + prow mr) & (cpp-1)
 int rw_conflicts(const RwGeo& g, int S, int tw, int mb, int npg, int sh, int mr) {
     static const int grp[4][16] = {{0, 1, 2, 3, 12, 13, 14, 15, 20, 21, 22, 23, 24, 25, 26, 27},
                                    {4, 5, 6, 7, 8, 9, 10, 11, 16, 17, 18, 19, 28, 29, 30, 31},
@@ -607,8 +622,10 @@ int rw_conflicts(const RwGeo& g, int S, int tw, int mb, int npg, int sh, int mr)
                             const int lane = grp[q][u], h = lane >> 5, r = lane & 31;
                             const int px = (pgi * mb + j) * 32 + r;
                             const int prow = S * (px / tw) + t / 3, pcol = S * (px % tw) + t % 3;
-                            const int f = ((pcol >> sh) + prow * mr) & (cpp - 1);
-                            const long long a = ((long long)(prow * g.pc + pcol) * cpp + ((2 * cb + h) ^ f)) * 16;
+                            // the kernel's LDS column (rw_lcol: stride 2 de-interleaves a patch row)
+                            const int lcol = S == 2 ? ((pcol & 1) ? (g.pc + 1) / 2 + (pcol >> 1) : (pcol >> 1)) : pcol;
+                            const int f = ((lcol >> sh) + prow * mr) & (cpp - 1);
+                            const long long a = ((long long)(prow * g.pc + lcol) * cpp + ((2 * cb + h) ^ f)) * 16;
                             const int slot = (int)((a / 16) & 15);
                             bool dup = false;
                             for (int k = 0; k < cnt[slot]; ++k) dup |= seen[slot][k] == a;
