@@ -118,6 +118,7 @@ def roofline(eng, args, batch, prof_steps, x, y):
                            for k, c in by_cls.items()})
 
 
+PMC_ROUND = "r06"   # this round's committed PMC summaries (copies of the tools/pmc_*.sh outputs) come first
 PMC_SUMMARY = os.path.join(ROOT, "profiles", "pmc_traffic_latest.json")
 TRACE_PROFILE = "profiles/r06_fwd_trace_ops.txt"   # rocprofv3 per-dispatch trace of this round's library
 
@@ -126,12 +127,14 @@ def pmc_traffic(cls, args):
     """HBM bytes per launch of kernel family `cls` from the committed rocprofv3 PMC summary
     (FETCH_SIZE / WRITE_SIZE passes over tools/pmc_run.py, corrected per the gfx950 guide by
     tools/pmc_traffic.py); bench.py cannot collect PMC counters from inside its own process.
-    profiles/pmc_traffic_latest.json (the headline configuration) or, for the other configs,
-    profiles/pmc_traffic_<variant>_<size>_b<batch>_<dtype>.json (tools/pmc_config.sh).
-    None unless a summary was collected on this bench's configuration."""
+    profiles/<round>_pmc_traffic.json / pmc_traffic_latest.json (the headline configuration) or,
+    for the other configs, profiles/[<round>_]pmc_traffic_<variant>_<size>_b<batch>_<dtype>.json
+    (tools/pmc_config.sh). None unless a summary was collected on this bench's configuration."""
     want = (args.variant, args.size, args.batch, args.dtype)
-    per_cfg = os.path.join(ROOT, "profiles", "pmc_traffic_%s_%d_b%d_%s.json" % want)
-    for path in (PMC_SUMMARY, per_cfg):
+    cfg_name = "pmc_traffic_%s_%d_b%d_%s.json" % want
+    prof = os.path.join(ROOT, "profiles")
+    for path in (os.path.join(prof, PMC_ROUND + "_pmc_traffic.json"), PMC_SUMMARY,
+                 os.path.join(prof, PMC_ROUND + "_" + cfg_name), os.path.join(prof, cfg_name)):
         try:
             with open(path) as f:
                 rec = json.load(f)
