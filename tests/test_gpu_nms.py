@@ -140,3 +140,23 @@ def test_negative_iou_threshold_vs_oracle(gpu, iou):
     y[:, 4:] = (1 / (1 + np.exp(-rng.normal(-5, 2.5, size=(B, nc, A))))).astype(np.float32)
     want = onms.non_max_suppression(y, 0.001, iou, 300, 30000)
     _assert_same(_gpu_nms(torch.from_numpy(y), gpu, iou_threshold=iou), want)
+
+
+@pytest.mark.parametrize("scores", ["spread", "tied"])
+def test_few_kept_long_continuation_vs_oracle(gpu, scores):
+    """Boxes of each class piled on one spot: an image keeps about one box per class of 67 k
+    candidates, so NMS runs later batches until max_nms candidates are processed (the C5
+    pattern). 'spread': scores over many bins (the fast path's compact list); 'tied': one score
+    for every pair (a single bin past 4096 keys: the radix-select path and its list)."""
+    rng = np.random.default_rng(21)
+    B, A, nc = 2, 8400, 8
+    y = np.empty((B, 4 + nc, A), np.float32)
+    y[:, 0:2] = 320.0 + rng.uniform(-2, 2, size=(B, 2, A))
+    y[:, 2:4] = 100.0 + rng.uniform(-2, 2, size=(B, 2, A))
+    if scores == "spread":
+        y[:, 4:] = rng.uniform(0.01, 0.99, size=(B, nc, A)).astype(np.float32)
+    else:
+        y[:, 4:] = 0.5
+    for kw in (dict(), dict(max_nms=50000, max_det=5)):
+        want = onms.non_max_suppression(y, 0.001, 0.65, kw.get("max_det", 300), kw.get("max_nms", 30000))
+        _assert_same(_gpu_nms(torch.from_numpy(y), gpu, **kw), want)

@@ -1,5 +1,7 @@
 """Phase timing of the NMS kernels on a real v11_n bf16 head output (debug hook yh_debug_nms_trace).
 
+  python tools/nms_trace.py [variant size batch dtype [scene seed]]
+
 Needs the diagnostic build of the library: make EXTRA=-DYH_ABLATION OUT=exp_lib/libyolo_hip.so
 OBJDIR=build/abl, then run with YH_LIB=exp_lib/libyolo_hip.so."""
 import ctypes
@@ -19,15 +21,19 @@ from yolo_hip.engine import Engine, nms  # noqa: E402
 
 def main():
     from nets import nn
-    B = 32
+    v = sys.argv[1] if len(sys.argv) > 1 else "n"
+    S = int(sys.argv[2]) if len(sys.argv) > 2 else 640
+    B = int(sys.argv[3]) if len(sys.argv) > 3 else 32
+    dt = {"bf16": torch.bfloat16, "fp16": torch.float16}[sys.argv[4] if len(sys.argv) > 4 else "bf16"]
+    seed = int(sys.argv[5]) if len(sys.argv) > 5 else 100
     torch.manual_seed(0)
-    model = nn.yolo_v11_n(80)
+    model = getattr(nn, f"yolo_v11_{v}")(80)
     model.load_state_dict(synth.synth_state_dict(model.state_dict(), seed=0))
     model.eval()
     dev = torch.device("cuda", 0)
-    eng = Engine(*model._yh_arch, dev, torch.bfloat16)
+    eng = Engine(*model._yh_arch, dev, dt)
     eng.load_module(model)
-    x = synth.synth_scenes(B, 640, 640, seed=100).to(dev, torch.bfloat16)
+    x = synth.synth_scenes(B, S, S, seed=seed).to(dev, dt)
     y = eng.forward(x)
     for _ in range(3):
         nms(y)
@@ -60,6 +66,11 @@ def main():
               f"sort {(r[11] - r[9]) / 100:.2f} sb0 decode {(r[12] - r[11]) / 100:.2f} sb0 kept+pairwise "
               f"{(r[13] - r[12]) / 100:.2f} sb0 resolve {(r[14] - r[13]) / 100:.2f} sb0 out {(r[15] - r[14]) / 100:.2f} "
               f"rest {(r[6] - r[15]) / 100:.2f}")
+    for i in range(B):
+        if t[i, 8] > 0:   # continued past the first batch: fast-path totals (slots 12 / 13)
+            g, r = int(t[i, 12]), int(t[i, 13])
+            print(f"image {i}: later batches {r >> 40}, gather (score scans) {g / 100:.1f} us, "
+                  f"sort + greedy {(r & ((1 << 40) - 1)) / 100:.1f} us, finish total {(t[i, 6] - t[i, 4]).item() / 100:.1f} us")
     print("kernel spans us: prep", ((t[:, 3] - t[:, 0]).max().item() * 10 / 1e3),
           "finish", ((t[:, 6] - t[:, 4]).max().item() * 10 / 1e3),
           "prep end -> finish start", ((t[:, 4].min() - t[:, 3].max()).item() * 10 / 1e3))
