@@ -66,11 +66,6 @@ def main():
               f"sort {(r[11] - r[9]) / 100:.2f} sb0 decode {(r[12] - r[11]) / 100:.2f} sb0 kept+pairwise "
               f"{(r[13] - r[12]) / 100:.2f} sb0 resolve {(r[14] - r[13]) / 100:.2f} sb0 out {(r[15] - r[14]) / 100:.2f} "
               f"rest {(r[6] - r[15]) / 100:.2f}")
-    for i in range(B):
-        if t[i, 8] > 0:   # continued past the first batch: fast-path totals (slots 12 / 13)
-            g, r = int(t[i, 12]), int(t[i, 13])
-            print(f"image {i}: later batches {r >> 40}, gather (score scans) {g / 100:.1f} us, "
-                  f"sort + greedy {(r & ((1 << 40) - 1)) / 100:.1f} us, finish total {(t[i, 6] - t[i, 4]).item() / 100:.1f} us")
     print("kernel spans us: prep", ((t[:, 3] - t[:, 0]).max().item() * 10 / 1e3),
           "finish", ((t[:, 6] - t[:, 4]).max().item() * 10 / 1e3),
           "prep end -> finish start", ((t[:, 4].min() - t[:, 3].max()).item() * 10 / 1e3))
