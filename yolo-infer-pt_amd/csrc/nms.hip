@@ -385,8 +385,19 @@ __device__ void nms_batch(NmsSmem& S, const NmsArgs& p, const T* y, float* dets,
         const int n = blockIdx.x;
         int sbi = 0;
         const IouThr th = make_thr(p.iou);
-#define SB_MARK(k) do { if (NMS_TRACE && tid == 0 && sbi == 0) NMS_TRACE[n * 16 + (k)] = __builtin_amdgcn_s_memrealtime(); } while (0)
+        // diagnostic builds: ticks of each part summed over all sub-batches (slots 12 decode, 13 kept
+        // test + pairwise mask, 14 resolve, 15 outputs; 15's bits 40+ count the sub-batches)
+        unsigned long long tprev = 0;
+#define SB_MARK(k)                                                                               \
+    do {                                                                                         \
+        if (NMS_TRACE && tid == 0) {                                                             \
+            const unsigned long long t_ = __builtin_amdgcn_s_memrealtime();                      \
+            if ((k) >= 12) NMS_TRACE[n * 16 + (k)] += t_ - tprev + ((k) == 15 ? (1ull << 40) : 0ull); \
+            tprev = t_;                                                                          \
+        }                                                                                        \
+    } while (0)
         for (int s0 = 0; s0 < want && S.kept < p.max_det; s0 += SB) {
+            SB_MARK(0);
             const int ns = min(SB, want - s0);
             float lo = INFINITY, hi = -INFINITY;
             bool fin = true;
@@ -895,7 +906,6 @@ __device__ void nms_rest(NmsSmem& S, const NmsArgs& p, const T* y, float* dets,
     }
     __syncthreads();
     NMS_MARK(8);
-    int nb2 = 0;
     // ---- fast path: batches of whole score bins, ~1024..CAP keys, exact order by an LDS sort
     while (!fallback && processed < ktot && S.kept < p.max_det && bin_hi >= 0) {
         const unsigned c0 = C[bin_hi + 1];
@@ -926,26 +936,31 @@ __device__ void nms_rest(NmsSmem& S, const NmsArgs& p, const T* y, float* dets,
         }
         if (tid == 0) S.gcount = 0;
         __syncthreads();
+        const unsigned long long tg0 = NMS_TRACE ? __builtin_amdgcn_s_memrealtime() : 0ull;
         gather_pairs<T, 2>(S, p, y, 0, nu, tid, [&](unsigned long long k) {
             const int bb = score_bin(__uint_as_float((unsigned)(k >> PBITS)), p.bin_base);
             return bb > blo && bb <= bin_hi;
         });
         __syncthreads();
-        if (nb2 == 0) NMS_MARK(9);
+        // diagnostic builds: slot 9 sums the batches' score scans (bits 40+: batches), 11 their sorts
+        const unsigned long long tg1 = NMS_TRACE ? __builtin_amdgcn_s_memrealtime() : 0ull;
         const int want = min(bcnt, ktot - processed);
         sort_batch(S, bcnt, tid);
-        if (nb2 == 0) NMS_MARK(11);
+        if (NMS_TRACE && tid == 0) {
+            NMS_TRACE[n * 16 + 9] += tg1 - tg0 + (1ull << 40);
+            NMS_TRACE[n * 16 + 11] += __builtin_amdgcn_s_memrealtime() - tg1;
+        }
         nms_batch<T>(S, p, y, dets, want, tid, lane, wave);
         processed += want;
         ub = S.bkeys[want - 1];
         bin_hi = blo;
-        ++nb2;
         __syncthreads();
     }
     if (fallback) {
         // ---- general path: radix-select the next <= CAP keys below ub (exact for any ties)
         while (processed < ktot && S.kept < p.max_det) {
             int want = min(CAP, ktot - processed);
+            const unsigned long long tf0 = NMS_TRACE ? __builtin_amdgcn_s_memrealtime() : 0ull;
             if (tid == 0) S.gcount = 0;
             __syncthreads();
             {
@@ -1010,7 +1025,12 @@ __device__ void nms_rest(NmsSmem& S, const NmsArgs& p, const T* y, float* dets,
             __syncthreads();
             gather_pairs<T, 2>(S, p, y, 0, nu, tid, [&](unsigned long long k) { return k >= lo && k < ub; });
             __syncthreads();
+            const unsigned long long tf1 = NMS_TRACE ? __builtin_amdgcn_s_memrealtime() : 0ull;
             sort_batch(S, want, tid);
+            if (NMS_TRACE && tid == 0) {
+                NMS_TRACE[n * 16 + 9] += tf1 - tf0 + (1ull << 40);
+                NMS_TRACE[n * 16 + 11] += __builtin_amdgcn_s_memrealtime() - tf1;
+            }
             nms_batch<T>(S, p, y, dets, want, tid, lane, wave);
             processed += want;
             ub = lo;
