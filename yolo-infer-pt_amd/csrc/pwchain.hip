@@ -133,8 +133,8 @@ __global__ __launch_bounds__(PWC_THREADS) void pw_chain(const PwChainArgs A) {
     // a two-step ring of A fragments: step k's in ring[k & 1], step k + 1's in flight
     uint4 ring[2][8];
     if (ps < A.nst) load_a(ps, pu, ppc, ring[0]);   // in flight with the prologue's DMAs
-    advance();
-    if (ps < A.nst) load_a(ps, pu, ppc, ring[1]);
+    advance();   // (step 1's fragments are requested after the prologue's barrier: the prologue
+                 // then waits for 64 KB less per workgroup, the CU's L2 intake being its bound)
     int kstep = 0;
     PWC_STAMP(24, false);
 
@@ -175,6 +175,7 @@ __global__ __launch_bounds__(PWC_THREADS) void pw_chain(const PwChainArgs A) {
     PWC_STAMP(27, false);
     pc_barrier();
     PWC_STAMP(1, false);
+    if (ps < A.nst) load_a(ps, pu, ppc, ring[1]);
 
     for (int s = 0; s < A.nst; ++s) {
         const PwcStage& S = A.st[s];
