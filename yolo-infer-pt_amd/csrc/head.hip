@@ -132,7 +132,7 @@ template <typename T>
 __device__ __forceinline__ void hc_dw(const T* src, int SW, int ss, T* dst, int DH, int DW, int ds, int c_lo, int C,
                                       const float* w, int wld, const float* b) {
     const int nrb = (DH + HC_RB - 1) / HC_RB, per_g = DW * nrb, ng = C >> 2;
-    const HcDiv dg = hc_div(per_g, 24), dw = hc_div(DW, 16);   // q < 2^24 / per_g: ng <= 64 groups
+    const HcDiv dw = hc_div(DW, 16);
     const int rs = SW * ss;                                      // one source row (elements)
     // the first item's weights are loaded before the barrier that opens the phase
     float4 wt[9], bb;
@@ -145,10 +145,14 @@ __device__ __forceinline__ void hc_dw(const T* src, int SW, int ss, T* dst, int 
         wg = g;
     };
     hc_barrier();   // src (and the parameters in LDS) complete
-    if ((int)threadIdx.x < ng * per_g) load_w(threadIdx.x / per_g);
+    // channel group fastest: the lanes of a wave read consecutive 8-B groups of one or two pixels
+    // (with the column fastest, lanes 16 apart hit one bank at the 144-B pixel stride: 37 % of
+    // head_cls's LDS cycles were bank conflicts, profiles/r06_sq_all_ops_c2.txt)
+    const HcDiv dn = hc_div(ng, 24);
+    if ((int)threadIdx.x < ng * per_g) load_w((int)threadIdx.x - hc_q(threadIdx.x, dn) * ng);
     for (int q = threadIdx.x; q < ng * per_g; q += HEAD_CLS_THREADS) {
-        const int g = hc_q(q, dg), rem = q - g * per_g;
-        const int rb = hc_q(rem, dw), c = rem - rb * DW;
+        const int p = hc_q(q, dn), g = q - p * ng;
+        const int rb = hc_q(p, dw), c = p - rb * DW;
         const int r0 = rb * HC_RB, c0 = c_lo + g * 4;
         if (g != wg) load_w(g);
         // rows past the source's last (DH + 1) read that row (outputs discarded below)
@@ -655,7 +659,10 @@ static bool hc_div_exact(int TH, int TW, int C0, int c3, int nc) {
     for (int k = 0; k < 2; ++k) {   // the two depthwise phases: MH x MW (dw1) and TH x TW (dw2)
         const long long DH = k ? TH : MH, DW = k ? TW : MW, ng = k ? ng2 : ng1;
         const long long per_g = DW * ((DH + HC_RB - 1) / HC_RB);
-        if (DW * per_g >= (1 << 16) || ng * per_g * per_g >= (1 << 24)) return false;
+        // item q < ng * per_g: q / ng (2^24 scale, n * m < 2^32), then (q / ng) / DW (2^16 scale)
+        if (DW * per_g >= (1 << 16) || ng * ng * per_g >= (1 << 24) ||
+            per_g * (1ll << 24) + ng * per_g >= (1ll << 32))
+            return false;
     }
     const long long na = (std::max(c3, nc) + 31) / 32, nb = (MH * MW + 31) / 32;
     return na * nb * nb < (1 << 16);   // hc_pw_units: unit index / nb
