@@ -1444,7 +1444,12 @@ struct Net {
             if (ops[i].kind != OP_CONV || cands[i].size() < 2 || !act[i]) continue;
             int prev = (int)i - 1;
             while (prev >= 0 && !act[prev]) --prev;
-            std::vector<float> t_ms(cands[i].size(), 0.f);
+            // two interleaved rounds over the candidates, each candidate's faster round kept: one
+            // disturbed measurement (another lane's kernels, a clock step) no longer decides a
+            // layer's plan for the life of the engine (a bench's roofline forward once read its
+            // 3x3 family 17 % slower than the same library's next run)
+            std::vector<float> t_ms(cands[i].size(), 3.0e38f);
+            for (int round = 0; round < 2; ++round)
             for (size_t c = 0; c < cands[i].size(); ++c) {
                 const MxPlan& pl = cands[i][c];
                 int rc = launch_mx_op(ops[i], pl, B, H, W, s);
@@ -1474,7 +1479,7 @@ struct Net {
                 if (tune_log)
                     fprintf(stderr, "[yh tune] %-36s %-40s %8.2f us\n", ops[i].label.c_str(), mx_name(pl).c_str(),
                             ms * 1e3f / 3);
-                t_ms[c] = ms;
+                t_ms[c] = std::min(t_ms[c], ms);
             }
             // pick after every candidate is timed: the fastest, except that for 3x3 layers a plan
             // within 3 % of the fastest that re-reads fewer input bytes (halo and cout-slice
